@@ -1,0 +1,35 @@
+// brr_launch.hpp -- host-callable launch wrappers for the kernels in brr_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "brr_device.hpp"
+
+namespace brr {
+
+enum RowFlagsHost : int {
+  H_ROW_SHIFT = 1, H_ROW_PENDING = 2, H_ROW_WRITE = 4, H_ROW_SNAPSHOT = 8, H_ROW_DEPS = 16,
+  H_ROW_EXCHANGE = 32, H_ROW_REDUCE = 64, H_ROW_INIT_Y = 128
+};
+enum MarkerModeHost : int { H_MR_BAYESR = 0, H_MR_HS = 1, H_MR_COUNT_ALL = 2 };
+
+hipError_t launch_synth_x(float *X, int64_t ld, int64_t N, int64_t M, int64_t col0, uint64_t ds,
+                          hipStream_t st);
+hipError_t launch_synth_y(const float *X, int64_t ld, int64_t N, const int *cidx, const double *cb,
+                          int nc, double *y, hipStream_t st);
+hipError_t launch_cast_x(const void *src, bool is_f64, int64_t lds, float *dst, int64_t ldd,
+                         int64_t N, int64_t M, hipStream_t st);
+hipError_t launch_gram(const Dev &d, int nblocks, hipStream_t st);
+hipError_t launch_xsq(const Dev &d, hipStream_t st);
+hipError_t launch_rows(const Dev &d, int flags, const double *deps_in, hipStream_t st);
+hipError_t launch_sweep_start(const Dev &d, uint32_t it, hipStream_t st);
+hipError_t launch_perm(const Dev &d, uint32_t it, int shard, bool identity, hipStream_t st);
+hipError_t launch_fixed(const Dev &d, uint32_t it, bool perm_on_device, hipStream_t st);
+hipError_t launch_stream(const Dev &d, int s, hipStream_t st);
+hipError_t launch_solve(const Dev &d, int s, uint32_t it, hipStream_t st);
+hipError_t set_solve_lds_limit(int B);
+size_t solve_lds_bytes(int B);
+hipError_t launch_markers(const Dev &d, int mode, uint32_t it, hipStream_t st);
+hipError_t launch_hyper(const Dev &d, uint32_t it, const double *stats, hipStream_t st);
+hipError_t launch_hyper_init(const Dev &d, const double *stats, bool pi_given, hipStream_t st);
+
+}  // namespace brr

@@ -1,0 +1,895 @@
+// brr_session.cpp -- host driver and C ABI (include/brr.h) of the MI355X Gibbs sampler.
+//
+// One brr_session = one chain on one GPU (one column shard).  Everything numeric runs in the
+// HIP kernels of brr_kernels.hip; the host only orders launches, moves data at the boundary,
+// and (for the reference visit order only) replays glibc rand() + std::random_shuffle.
+// There is no CPU compute fallback: without a usable HIP device every entry point fails.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "../../include/brr.h"
+#include "brr_device.hpp"
+#include "brr_launch.hpp"
+#include "brr_rng.hpp"
+
+using namespace brr;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct Logger {
+  brr_log_fn fn = nullptr;
+  void *user = nullptr;
+  void operator()(const char *fmt, ...) const {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (fn) fn(buf, user); else fputs(buf, stderr);
+  }
+};
+
+#define HIPCHK(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      set_error("HIP error %s at %s:%d: %s", hipGetErrorString(e_), __FILE__, __LINE__, \
+                #expr);                                                                \
+      return -2;                                                                       \
+    }                                                                                  \
+  } while (0)
+
+void set_error(const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+}
+
+// glibc rand() (random_r TYPE_3) from a fresh-process state, and libstdc++'s
+// std::random_shuffle (/usr/include/c++/11/bits/stl_algo.h:4568-4582) -- the reference's
+// visit order (BayesRv2.cpp:182), used by BRR_ORDER_REFERENCE.
+struct GlibcRand {
+  int32_t r[34];
+  int idx = 0;
+  void seed(uint32_t s) {
+    int32_t x[344];
+    if (s == 0) s = 1;
+    x[0] = (int32_t)s;
+    for (int i = 1; i < 31; ++i) {
+      const int32_t hi = x[i - 1] / 127773, lo = x[i - 1] % 127773;
+      int32_t word = 16807 * lo - 2836 * hi;
+      if (word < 0) word += 2147483647;
+      x[i] = word;
+    }
+    for (int i = 31; i < 34; ++i) x[i] = x[i - 31];
+    for (int i = 34; i < 344; ++i) x[i] = (int32_t)((uint32_t)x[i - 31] + (uint32_t)x[i - 3]);
+    for (int i = 0; i < 34; ++i) r[i] = x[310 + i];
+    idx = 0;
+  }
+  int32_t next() {
+    const int32_t v = (int32_t)((uint32_t)r[(idx + 3) % 34] + (uint32_t)r[(idx + 31) % 34]);
+    r[idx] = v;
+    idx = (idx + 1) % 34;
+    return (int32_t)((uint32_t)v >> 1);
+  }
+  void shuffle(std::vector<int32_t> &a) {
+    for (size_t i = 1; i < a.size(); ++i) {
+      const size_t j = (size_t)(next() % (int32_t)(i + 1));
+      if (i != j) std::swap(a[i], a[j]);
+    }
+  }
+};
+
+template <class T>
+int dalloc(T **p, int64_t n) {
+  *p = nullptr;
+  if (n <= 0) n = 1;
+  hipError_t e = hipMalloc((void **)p, sizeof(T) * (size_t)n);
+  if (e != hipSuccess) {
+    set_error("hipMalloc(%lld bytes) failed: %s", (long long)(sizeof(T) * n), hipGetErrorString(e));
+    return -2;
+  }
+  return 0;
+}
+
+}  // namespace
+
+struct brr_session {
+  brr_options opt;
+  Logger log;
+  Dev d{};
+  int device = 0;
+  hipStream_t st = nullptr;
+  int64_t N = 0, M = 0, M_total = 0, col_offset = 0;
+  int K = 1, G = 1, F = 0, B = 128, nb = 0, model = 0, NS = 0;
+  int order_mode = BRR_ORDER_BLOCKED;
+  int shard = 0, nshard = 1;
+  int32_t iteration = 0;
+  bool initialized = false, pi_given = false, need_reduce = false, have_y = false, have_x = false;
+  double mu0 = 0, sigmaE0 = 0;
+  double *ex_eps = nullptr, *ex_stats = nullptr;  // exchange buffers (caller- or session-owned)
+  bool ex_owned = false;
+  std::vector<double> synth_y;  // this shard's X_causal beta_causal (synthetic cohort)
+  ncclComm_t comm = nullptr;
+  // reference visit order state
+  GlibcRand grand;
+  std::vector<int32_t> ref_order, ref_forder;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  std::vector<std::pair<size_t, int>> ev_pairs;  // (start index, kind 0=stream 1=solve)
+  double t_stream = 0, t_solve = 0;
+  int64_t n_stream = 0, n_solve = 0;
+  std::vector<void *> allocs;
+
+  template <class T>
+  int alloc(T **p, int64_t n) {
+    int rc = dalloc(p, n);
+    if (rc == 0) allocs.push_back((void *)*p);
+    return rc;
+  }
+  ~brr_session() {
+    if (st) (void)hipStreamSynchronize(st);
+    if (comm) (void)ncclCommDestroy(comm);
+    for (void *p : allocs) (void)hipFree(p);
+    for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
+    if (st) (void)hipStreamDestroy(st);
+  }
+  hipEvent_t ev() {
+    if (ev_used == ev_pool.size()) {
+      hipEvent_t e;
+      (void)hipEventCreate(&e);
+      ev_pool.push_back(e);
+    }
+    return ev_pool[ev_used++];
+  }
+};
+
+namespace {
+
+int rows_flagged(brr_session *s, int flags, const double *deps_in = nullptr) {
+  HIPCHK(launch_rows(s->d, flags, deps_in, s->st));
+  return 0;
+}
+
+int collect_timing(brr_session *s) {
+  if (s->ev_pairs.empty()) return 0;
+  HIPCHK(hipStreamSynchronize(s->st));
+  for (auto &pr : s->ev_pairs) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, s->ev_pool[pr.first], s->ev_pool[pr.first + 1]));
+    if (pr.second == 0) { s->t_stream += ms; s->n_stream++; } else { s->t_solve += ms; s->n_solve++; }
+  }
+  s->ev_pairs.clear();
+  s->ev_used = 0;
+  return 0;
+}
+
+int upload_order(brr_session *s, const std::vector<int32_t> &order) {
+  // positions s*B+i of the reference order; Gram blocks follow the positions
+  std::vector<int32_t> mem((size_t)s->nb * s->B, 0), gi((size_t)s->nb * s->B, 0), bsz(s->nb), gb(s->nb);
+  for (int b = 0; b < s->nb; ++b) {
+    const int size = (int)std::min<int64_t>(s->B, s->M - (int64_t)b * s->B);
+    bsz[b] = size;
+    gb[b] = b;
+    for (int i = 0; i < size; ++i) {
+      mem[(size_t)b * s->B + i] = order[(size_t)b * s->B + i];
+      gi[(size_t)b * s->B + i] = i;
+    }
+  }
+  HIPCHK(hipMemcpyAsync(s->d.member, mem.data(), mem.size() * 4, hipMemcpyHostToDevice, s->st));
+  HIPCHK(hipMemcpyAsync(s->d.gidx, gi.data(), gi.size() * 4, hipMemcpyHostToDevice, s->st));
+  HIPCHK(hipMemcpyAsync(s->d.bsz, bsz.data(), bsz.size() * 4, hipMemcpyHostToDevice, s->st));
+  HIPCHK(hipMemcpyAsync(s->d.gblk, gb.data(), gb.size() * 4, hipMemcpyHostToDevice, s->st));
+  HIPCHK(hipStreamSynchronize(s->st));  // host vectors go out of scope
+  return 0;
+}
+
+int ensure_reduced(brr_session *s) {
+  if (!s->need_reduce) return 0;
+  s->need_reduce = false;
+  return rows_flagged(s, H_ROW_REDUCE);
+}
+
+int do_sweep_local(brr_session *s) {
+  if (!s->initialized) { set_error("session not initialised (brr_session_init)"); return -1; }
+  if (int rc = ensure_reduced(s)) return rc;
+  const uint32_t it = (uint32_t)s->iteration;
+  const bool sharded = s->nshard > 1;
+  Dev &d = s->d;
+  HIPCHK(launch_sweep_start(d, it, s->st));
+  if (int rc = rows_flagged(s, H_ROW_SHIFT | H_ROW_WRITE)) return rc;
+  // visit order
+  if (s->order_mode == BRR_ORDER_BLOCKED) {
+    HIPCHK(launch_perm(d, it, s->shard, false, s->st));
+  } else if (s->order_mode == BRR_ORDER_REFERENCE) {
+    if (s->F > 0) {  // fixedI shuffled before markerI (BayesRv2Groups.cpp:216,227)
+      s->grand.shuffle(s->ref_forder);
+      HIPCHK(hipMemcpyAsync(d.forder, s->ref_forder.data(), (size_t)s->F * 4, hipMemcpyHostToDevice, s->st));
+    }
+    s->grand.shuffle(s->ref_order);
+    if (int rc = upload_order(s, s->ref_order)) return rc;
+    HIPCHK(launch_gram(d, s->nb, s->st));
+  } else {
+    HIPCHK(launch_perm(d, it, s->shard, true, s->st));
+  }
+  if (s->model == MODEL_GROUPS && s->F > 0)
+    HIPCHK(launch_fixed(d, it, s->order_mode == BRR_ORDER_BLOCKED, s->st));
+  if (sharded)
+    if (int rc = rows_flagged(s, H_ROW_SNAPSHOT)) return rc;
+  // the hot loop: one streaming pass + one solve per block of B markers
+  for (int b = 0; b < s->nb; ++b) {
+    if (s->timing) {
+      const size_t i0 = s->ev_used;
+      hipEvent_t e0 = s->ev(), e1 = s->ev();
+      HIPCHK(hipEventRecord(e0, s->st));
+      HIPCHK(launch_stream(d, b, s->st));
+      HIPCHK(hipEventRecord(e1, s->st));
+      s->ev_pairs.push_back({i0, 0});
+      const size_t i2 = s->ev_used;
+      hipEvent_t e2 = s->ev(), e3 = s->ev();
+      HIPCHK(hipEventRecord(e2, s->st));
+      HIPCHK(launch_solve(d, b, it, s->st));
+      HIPCHK(hipEventRecord(e3, s->st));
+      s->ev_pairs.push_back({i2, 1});
+    } else {
+      HIPCHK(launch_stream(d, b, s->st));
+      HIPCHK(launch_solve(d, b, it, s->st));
+    }
+  }
+  if (sharded) {
+    if (!s->ex_eps || !s->ex_stats) { set_error("exchange buffers not set"); return -1; }
+    Dev dx = d;
+    dx.deps = s->ex_eps;
+    HIPCHK(launch_rows(dx, H_ROW_PENDING | H_ROW_WRITE | H_ROW_DEPS, nullptr, s->st));
+  } else {
+    if (int rc = rows_flagged(s, H_ROW_PENDING | H_ROW_WRITE | H_ROW_REDUCE)) return rc;
+  }
+  const int mode = s->model == MODEL_HORSESHOE ? H_MR_HS : H_MR_BAYESR;
+  HIPCHK(launch_markers(d, mode, it, s->st));
+  if (sharded)
+    HIPCHK(hipMemcpyAsync(s->ex_stats, d.stats, sizeof(double) * s->NS, hipMemcpyDeviceToDevice, s->st));
+  return 0;
+}
+
+int do_sweep_finish(brr_session *s) {
+  const uint32_t it = (uint32_t)s->iteration;
+  const bool sharded = s->nshard > 1;
+  if (sharded) {
+    if (int rc = rows_flagged(s, H_ROW_EXCHANGE | H_ROW_WRITE | H_ROW_REDUCE, s->ex_eps)) return rc;
+    HIPCHK(launch_hyper(s->d, it, s->ex_stats, s->st));
+  } else {
+    HIPCHK(launch_hyper(s->d, it, s->d.stats, s->st));
+  }
+  s->iteration++;
+  if (s->timing) return collect_timing(s);
+  return 0;
+}
+
+template <class T>
+int h2d(brr_session *s, T *dst, const T *src, int64_t n) {
+  if (n <= 0) return 0;
+  HIPCHK(hipMemcpyAsync(dst, src, sizeof(T) * (size_t)n, hipMemcpyHostToDevice, s->st));
+  HIPCHK(hipStreamSynchronize(s->st));
+  return 0;
+}
+
+template <class T>
+int d2h(brr_session *s, T *dst, const T *src, int64_t n) {
+  if (n <= 0) return 0;
+  HIPCHK(hipStreamSynchronize(s->st));
+  HIPCHK(hipMemcpy(dst, src, sizeof(T) * (size_t)n, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+}  // namespace
+
+// =======================================================================================
+extern "C" {
+
+void brr_options_default(brr_options *o) {
+  std::memset(o, 0, sizeof *o);
+  o->abi_version = BRR_ABI_VERSION;
+  o->block_size = 128;
+  o->order_mode = BRR_ORDER_BLOCKED;
+  o->shard_count = 1;
+}
+
+const char *brr_last_error(void) { return g_last_error.c_str(); }
+
+int brr_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_total,
+                                int64_t col_offset, int32_t K, int32_t groups, int64_t F,
+                                const brr_options *opt_in) {
+  brr_options opt;
+  if (opt_in) opt = *opt_in; else brr_options_default(&opt);
+  if (model < 0 || model > 3) { set_error("bad model %d", model); return nullptr; }
+  if (N < 1 || M < 1) { set_error("N and M must be >= 1"); return nullptr; }
+  if (M_total < M) M_total = M;
+  if (model == MODEL_HORSESHOE) K = 1;
+  if (K < 1 || K > MAXK) { set_error("mixture components K=%d outside [1,%d]", K, MAXK); return nullptr; }
+  if (model == MODEL_V2 || model == MODEL_HORSESHOE) groups = 1;
+  if (groups < 1 || groups > MAXG) { set_error("groups=%d outside [1,%d]", groups, MAXG); return nullptr; }
+  if (model != MODEL_GROUPS) F = 0;
+  if (F < 0 || F > 1024) { set_error("fixed effects F=%lld outside [0,1024]", (long long)F); return nullptr; }
+  int B = opt.block_size > 0 ? opt.block_size : 128;
+  if (B % 64 != 0 || B > BMAX) { set_error("block_size=%d must be a multiple of 64 and <= %d", B, BMAX); return nullptr; }
+  if (opt.shard_count < 1) opt.shard_count = 1;
+  if (opt.shard_count > 1 && (col_offset % B) != 0) {
+    set_error("col_offset must be a multiple of block_size when sharded");
+    return nullptr;
+  }
+  if (opt.shard_count > 1 && opt.order_mode == BRR_ORDER_REFERENCE) {
+    set_error("the reference visit order is defined for a single shard only");
+    return nullptr;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+    set_error("no HIP device available: the MI355X sampler has no CPU fallback");
+    return nullptr;
+  }
+  if (opt.device < 0 || opt.device >= ndev) { set_error("device %d not present", opt.device); return nullptr; }
+  brr_session *s = new brr_session();
+  s->opt = opt;
+  s->log.fn = opt.log;
+  s->log.user = opt.log_userdata;
+  s->device = opt.device;
+  if (hipSetDevice(s->device) != hipSuccess || hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) {
+    set_error("cannot initialise HIP device %d", s->device);
+    delete s;
+    return nullptr;
+  }
+  hipDeviceProp_t prop;
+  (void)hipGetDeviceProperties(&prop, s->device);
+  const int cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  s->N = N; s->M = M; s->M_total = M_total; s->col_offset = col_offset;
+  s->K = K; s->G = groups; s->F = (int)F; s->B = B; s->model = model;
+  s->order_mode = opt.order_mode;
+  s->shard = opt.shard_rank; s->nshard = opt.shard_count;
+  s->nb = (int)((M + B - 1) / B);
+  s->NS = stats_size(groups, K);
+  Dev &d = s->d;
+  d.N = N; d.ld = (N + 63) / 64 * 64; d.M = M; d.M_total = M_total; d.col_offset = col_offset;
+  d.K = K; d.G = groups; d.F = (int)F; d.B = B; d.nb = s->nb; d.model = model;
+  // streaming geometry: ~2 workgroups per CU, one row per thread
+  const int64_t target = 2LL * cus;
+  d.R = (int)std::min<int64_t>(256, std::max<int64_t>(1, (N + target - 1) / target));
+  d.RG = (int)((N + d.R - 1) / d.R);
+  d.NG = (d.RG + STREAM_GROUP - 1) / STREAM_GROUP;
+  d.MRG = (int)((M + 255) / 256);
+  const int64_t RGrows = (N + 255) / 256;
+  int rc = 0;
+  rc |= s->alloc(const_cast<float **>(&d.X), d.ld * M);
+  rc |= s->alloc(const_cast<double **>(&d.Y), N);
+  rc |= s->alloc(const_cast<double **>(&d.fixed), N * std::max<int64_t>(F, 1));
+  rc |= s->alloc(const_cast<double **>(&d.cva), (int64_t)groups * std::max(K - 1, 1));
+  rc |= s->alloc(&d.eps, N);
+  rc |= s->alloc(&d.eps_start, N);
+  rc |= s->alloc(&d.beta, M);
+  rc |= s->alloc(&d.xsq, M);
+  rc |= s->alloc(&d.lambda, M);
+  rc |= s->alloc(&d.hsv, M);
+  rc |= s->alloc(&d.sigmaGG, groups);
+  rc |= s->alloc(&d.pi, (int64_t)groups * K);
+  rc |= s->alloc(&d.alpha, std::max<int64_t>(F, 1));
+  rc |= s->alloc(&d.comp, M);
+  rc |= s->alloc(&d.forder, std::max<int64_t>(F, 1));
+  rc |= s->alloc(&d.sel, M);
+  rc |= s->alloc(&d.gram, (int64_t)s->nb * B * B);
+  rc |= s->alloc(&d.member, (int64_t)s->nb * B);
+  rc |= s->alloc(&d.gidx, (int64_t)s->nb * B);
+  rc |= s->alloc(&d.bsz, s->nb);
+  rc |= s->alloc(&d.gblk, s->nb);
+  rc |= s->alloc(&d.blkorder, s->nb);
+  rc |= s->alloc(&d.slab1, (int64_t)d.RG * B);
+  rc |= s->alloc(&d.slab2, (int64_t)d.NG * B);
+  rc |= s->alloc(&d.cnt1, d.NG);
+  rc |= s->alloc(&d.pend_idx, B);
+  rc |= s->alloc(&d.pend_bo, B);
+  rc |= s->alloc(&d.pend_bn, B);
+  rc |= s->alloc(&d.rslab, 2 * RGrows);
+  rc |= s->alloc(&d.rcnt, 1);
+  rc |= s->alloc(&d.mslab, (int64_t)d.MRG * s->NS);
+  rc |= s->alloc(&d.mcnt, 1);
+  rc |= s->alloc(&d.stats, s->NS);
+  rc |= s->alloc(&d.sc, 1);
+  d.deps = nullptr;
+  if (rc) { delete s; return nullptr; }
+  d.gAssign = nullptr;
+  bool ok = hipMemsetAsync(d.cnt1, 0, sizeof(int) * d.NG, s->st) == hipSuccess &&
+            hipMemsetAsync(d.rcnt, 0, sizeof(int), s->st) == hipSuccess &&
+            hipMemsetAsync(d.mcnt, 0, sizeof(int), s->st) == hipSuccess &&
+            hipMemsetAsync(d.sc, 0, sizeof(Scal), s->st) == hipSuccess &&
+            hipMemsetAsync(d.stats, 0, sizeof(double) * s->NS, s->st) == hipSuccess &&
+            hipMemsetAsync(const_cast<float *>(d.X), 0, sizeof(float) * d.ld * M, s->st) == hipSuccess &&
+            hipMemsetAsync(d.alpha, 0, sizeof(double) * std::max<int64_t>(F, 1), s->st) == hipSuccess &&
+            hipMemsetAsync(const_cast<double *>(d.fixed), 0, sizeof(double) * N * std::max<int64_t>(F, 1), s->st) == hipSuccess &&
+            set_solve_lds_limit(B) == hipSuccess && hipStreamSynchronize(s->st) == hipSuccess;
+  if (!ok) { set_error("device initialisation failed"); delete s; return nullptr; }
+  if (groups > 1) {
+    int *ga = nullptr;
+    if (s->alloc(&ga, M)) { delete s; return nullptr; }
+    (void)hipMemsetAsync(ga, 0, sizeof(int) * M, s->st);
+    d.gAssign = ga;
+  }
+  s->ref_order.resize((size_t)M);
+  for (int64_t i = 0; i < M; ++i) s->ref_order[(size_t)i] = (int32_t)i;
+  s->ref_forder.resize((size_t)std::max(s->F, 0));
+  for (int i = 0; i < s->F; ++i) s->ref_forder[(size_t)i] = i;
+  s->grand.seed(1);  // a fresh process: rand() unseeded == srand(1)
+  return s;
+}
+
+void brr_session_destroy(brr_session *s) { delete s; }
+
+static int upload_x_any(brr_session *s, const void *X, bool f64, int64_t ldx) {
+  if (!s || !X) { set_error("null argument"); return -1; }
+  if (ldx < s->N) { set_error("ldx < N"); return -1; }
+  HIPCHK(hipSetDevice(s->device));
+  const size_t esz = f64 ? 8 : 4;
+  const int64_t chunk_cols = std::min<int64_t>(
+      65535, std::max<int64_t>(1, (int64_t)(256ll << 20) / (int64_t)(esz * ldx)));  // grid.y limit
+  void *stage = nullptr;
+  HIPCHK(hipMalloc(&stage, esz * (size_t)ldx * (size_t)std::min<int64_t>(chunk_cols, s->M)));
+  for (int64_t c0 = 0; c0 < s->M; c0 += chunk_cols) {
+    const int64_t nc = std::min<int64_t>(chunk_cols, s->M - c0);
+    hipError_t e = hipMemcpy(stage, (const char *)X + esz * (size_t)ldx * (size_t)c0, esz * (size_t)ldx * (size_t)nc,
+                             hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+      e = launch_cast_x(stage, f64, ldx, const_cast<float *>(s->d.X) + s->d.ld * c0, s->d.ld, s->N, nc, s->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->st);
+    if (e != hipSuccess) {
+      (void)hipFree(stage);
+      set_error("X upload failed: %s", hipGetErrorString(e));
+      return -2;
+    }
+  }
+  (void)hipFree(stage);
+  s->have_x = true;
+  return 0;
+}
+
+int brr_session_upload_x_f64(brr_session *s, const double *X, int64_t ldx) { return upload_x_any(s, X, true, ldx); }
+int brr_session_upload_x_f32(brr_session *s, const float *X, int64_t ldx) { return upload_x_any(s, X, false, ldx); }
+
+int brr_session_synthesize(brr_session *s, uint64_t ds, double h2, int64_t n_causal) {
+  if (!s) return -1;
+  HIPCHK(hipSetDevice(s->device));
+  HIPCHK(launch_synth_x(const_cast<float *>(s->d.X), s->d.ld, s->N, s->M, s->col_offset, ds, s->st));
+  s->have_x = true;
+  // this shard's genetic values X_c beta_c over its causal columns
+  if (n_causal < 1) n_causal = std::max<int64_t>(1, std::min<int64_t>(1000, s->M_total / 10));
+  const double pc = (double)n_causal / (double)s->M_total;
+  const double scale = std::sqrt(h2 / (double)n_causal);
+  std::vector<int> cidx;
+  std::vector<double> cb;
+  for (int64_t jl = 0; jl < s->M; ++jl) {
+    const int64_t j = s->col_offset + jl;
+    if (uniform(ds, T_DATA_FREQ, (uint32_t)j, 0, 1) < pc) {
+      cidx.push_back((int)jl);
+      cb.push_back(normal(ds, T_DATA_FREQ, (uint32_t)j, 0, 2) * scale);
+    }
+  }
+  int *dci = nullptr;
+  double *dcb = nullptr, *dy = nullptr;
+  const int nc = (int)cidx.size();
+  HIPCHK(hipMalloc(&dci, sizeof(int) * std::max(nc, 1)));
+  HIPCHK(hipMalloc(&dcb, sizeof(double) * std::max(nc, 1)));
+  HIPCHK(hipMalloc(&dy, sizeof(double) * s->N));
+  if (nc) {
+    HIPCHK(hipMemcpy(dci, cidx.data(), sizeof(int) * nc, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(dcb, cb.data(), sizeof(double) * nc, hipMemcpyHostToDevice));
+  }
+  HIPCHK(launch_synth_y(s->d.X, s->d.ld, s->N, dci, dcb, nc, dy, s->st));
+  s->synth_y.assign((size_t)s->N, 0.0);
+  HIPCHK(hipStreamSynchronize(s->st));
+  HIPCHK(hipMemcpy(s->synth_y.data(), dy, sizeof(double) * s->N, hipMemcpyDeviceToHost));
+  (void)hipFree(dci); (void)hipFree(dcb); (void)hipFree(dy);
+  if (s->nshard > 1) return 0;  // Y needs every shard's genetic values: brr_session_synth_y
+  return brr_session_synth_y(s, s->synth_y.data(), ds, h2);
+}
+
+int brr_session_synth_partial_y(brr_session *s, double *out) {
+  if (!s || !out || s->synth_y.size() != (size_t)s->N) { set_error("no synthetic genetic values"); return -1; }
+  std::memcpy(out, s->synth_y.data(), sizeof(double) * s->N);
+  return 0;
+}
+
+int brr_session_synth_y(brr_session *s, const double *g_sum, uint64_t ds, double h2) {
+  if (!s || !g_sum) return -1;
+  std::vector<double> y(g_sum, g_sum + s->N);
+  const double se = std::sqrt(1.0 - h2);
+  double mean = 0.0;
+  for (int64_t i = 0; i < s->N; ++i) {
+    y[(size_t)i] += se * normal(ds, T_DATA_NOISE, (uint32_t)i, 0, 0);
+    mean += y[(size_t)i];
+  }
+  mean /= (double)s->N;
+  double ss = 0.0;
+  for (int64_t i = 0; i < s->N; ++i) ss += (y[(size_t)i] - mean) * (y[(size_t)i] - mean);
+  const double sd = s->N > 1 ? std::sqrt(ss / (double)(s->N - 1)) : 1.0;
+  for (auto &v : y) v = (v - mean) / (sd > 0 ? sd : 1.0);  // Y = scale(y)
+  return brr_session_set_y(s, y.data());
+}
+
+int brr_session_set_y(brr_session *s, const double *Y) {
+  if (!s || !Y) return -1;
+  s->have_y = true;
+  return h2d(s, const_cast<double *>(s->d.Y), Y, s->N);
+}
+
+int brr_session_set_fixed(brr_session *s, const double *fixed) {
+  if (!s) return -1;
+  if (s->F == 0) return 0;
+  if (!fixed) return -1;
+  return h2d(s, const_cast<double *>(s->d.fixed), fixed, s->N * s->F);
+}
+
+int brr_session_set_bayesr(brr_session *s, double sigma0, double v0E, double s02E, double v0G,
+                           double s02G, const double *cva, const int32_t *gAssign) {
+  if (!s) return -1;
+  Hyper &h = s->d.hyp;
+  h.sigma0 = sigma0; h.v0E = v0E; h.s02E = s02E; h.v0G = v0G; h.s02G = s02G;
+  const int nc = s->K - 1;
+  if (nc > 0) {
+    if (!cva) { set_error("cva required"); return -1; }
+    if (int rc = h2d(s, const_cast<double *>(s->d.cva), cva, (int64_t)s->G * nc)) return rc;
+  }
+  if (s->G > 1) {
+    if (!gAssign) { set_error("gAssign required for groups > 1"); return -1; }
+    for (int64_t m = 0; m < s->M; ++m)
+      if (gAssign[m] < 0 || gAssign[m] >= s->G) { set_error("gAssign[%lld]=%d outside [0,%d)", (long long)m, gAssign[m], s->G); return -1; }
+    if (int rc = h2d(s, const_cast<int *>(s->d.gAssign), (const int *)gAssign, s->M)) return rc;
+  }
+  if (!s->pi_given) {  // priorPi (BayesRv2Groups.cpp:170-175; SURVEY Appendix B for V2)
+    std::vector<double> pi((size_t)s->G * s->K);
+    for (int g = 0; g < s->G; ++g) {
+      pi[(size_t)g * s->K] = 0.5;
+      for (int k = 1; k < s->K; ++k) pi[(size_t)g * s->K + k] = 0.5 / s->K;
+    }
+    if (int rc = h2d(s, s->d.pi, pi.data(), (int64_t)pi.size())) return rc;
+  }
+  return 0;
+}
+
+int brr_session_set_horseshoe(brr_session *s, double A, double v0E, double s02E, double vL,
+                              double vT, double c2, double vC, double sC) {
+  if (!s) return -1;
+  Hyper &h = s->d.hyp;
+  h.A = A; h.v0E = v0E; h.s02E = s02E; h.vL = vL; h.vT = vT; h.c2_0 = c2; h.vC = vC; h.sC = sC;
+  return 0;
+}
+
+int brr_session_set_restart(brr_session *s, double mu, const double *beta, double sigmaE,
+                            const double *sigmaGG, const double *eps, const double *comp) {
+  if (!s || !beta || !sigmaGG || !eps || !comp) { set_error("null argument"); return -1; }
+  std::vector<int> c((size_t)s->M);
+  for (int64_t m = 0; m < s->M; ++m) {
+    const int k = (int)comp[m];  // Eigen indexes v(g, components(i)) with a double
+    if (k < 0 || k >= s->K) { set_error("components[%lld]=%g outside [0,%d)", (long long)m, comp[m], s->K); return -1; }
+    c[(size_t)m] = k;
+  }
+  s->mu0 = mu;
+  s->sigmaE0 = sigmaE;
+  int rc = h2d(s, s->d.beta, beta, s->M);
+  rc = rc ? rc : h2d(s, s->d.comp, c.data(), s->M);
+  rc = rc ? rc : h2d(s, s->d.sigmaGG, sigmaGG, s->G);
+  rc = rc ? rc : h2d(s, s->d.eps, eps, s->N);
+  return rc;
+}
+
+int brr_session_set_pi(brr_session *s, const double *pi) {
+  if (!s || !pi) return -1;
+  s->pi_given = true;
+  return h2d(s, s->d.pi, pi, (int64_t)s->G * s->K);
+}
+
+int brr_session_init(brr_session *s, int32_t seed) {
+  if (!s) return -1;
+  if (!s->have_x) { set_error("X not uploaded"); return -1; }
+  if (s->model != MODEL_RESTART && !s->have_y) { set_error("Y not set"); return -1; }
+  HIPCHK(hipSetDevice(s->device));
+  Dev &d = s->d;
+  d.seed = (uint64_t)(int64_t)seed;
+  // identity block layout -> Gram blocks and xsquared (BayesRv2.cpp:170)
+  HIPCHK(launch_perm(d, 0, s->shard, true, s->st));
+  HIPCHK(launch_gram(d, s->nb, s->st));
+  HIPCHK(launch_xsq(d, s->st));
+  Scal sc{};
+  if (s->model == MODEL_RESTART) { sc.mu = s->mu0; sc.sigmaE = s->sigmaE0; }
+  if (s->model == MODEL_HORSESHOE) sc.c2 = d.hyp.c2_0;
+  HIPCHK(hipMemcpyAsync(d.sc, &sc, sizeof sc, hipMemcpyHostToDevice, s->st));
+  if (s->model != MODEL_RESTART) {
+    HIPCHK(hipMemsetAsync(d.beta, 0, sizeof(double) * s->M, s->st));
+    HIPCHK(hipMemsetAsync(d.comp, 0, sizeof(int) * s->M, s->st));
+  }
+  HIPCHK(hipMemsetAsync(d.sel, 0, s->M, s->st));
+  HIPCHK(hipMemsetAsync(d.alpha, 0, sizeof(double) * std::max(s->F, 1), s->st));
+  if (s->F > 0)  // identity fixed-effect order (IDENTITY mode; REFERENCE overwrites per sweep)
+    if (int rc = h2d(s, d.forder, s->ref_forder.data(), s->F)) return rc;
+  if (s->model == MODEL_HORSESHOE) {
+    std::vector<double> ones((size_t)s->M, 1.0);
+    if (int rc = h2d(s, d.lambda, ones.data(), s->M)) return rc;
+    if (int rc = h2d(s, d.hsv, ones.data(), s->M)) return rc;
+  }
+  if (int rc = rows_flagged(s, (s->model == MODEL_RESTART ? 0 : (H_ROW_INIT_Y | H_ROW_WRITE)) | H_ROW_REDUCE)) return rc;
+  if (s->model == MODEL_RESTART) {
+    HIPCHK(launch_markers(d, H_MR_COUNT_ALL, 0, s->st));
+    if (s->nshard > 1) { set_error("restart across shards needs summed counts: not supported"); return -1; }
+  }
+  HIPCHK(launch_hyper_init(d, d.stats, s->pi_given, s->st));
+  HIPCHK(hipStreamSynchronize(s->st));
+  s->iteration = 0;
+  s->initialized = true;
+  s->need_reduce = false;
+  return 0;
+}
+
+int brr_session_sweep(brr_session *s, int32_t n) {
+  if (!s) return -1;
+  if (s->nshard > 1 && !s->comm) {
+    set_error("sharded session without a communicator: brr_session_comm_init, or drive "
+              "sweep_local / exchange / sweep_finish yourself");
+    return -1;
+  }
+  HIPCHK(hipSetDevice(s->device));
+  for (int r = 0; r < n; ++r) {
+    if (int rc = do_sweep_local(s)) return rc;
+    if (s->nshard > 1) {
+      // the one exchange step of the column-sharded sweep: sum of residual deltas
+      // (N doubles) and of the marker statistics, in place, on the session stream
+      ncclResult_t r1 = ncclAllReduce(s->ex_eps, s->ex_eps, (size_t)s->N, ncclDouble, ncclSum, s->comm, s->st);
+      ncclResult_t r2 = ncclAllReduce(s->ex_stats, s->ex_stats, (size_t)s->NS, ncclDouble, ncclSum, s->comm, s->st);
+      if (r1 != ncclSuccess || r2 != ncclSuccess) {
+        set_error("ncclAllReduce failed: %s", ncclGetErrorString(r1 != ncclSuccess ? r1 : r2));
+        return -2;
+      }
+    }
+    if (int rc = do_sweep_finish(s)) return rc;
+  }
+  return 0;
+}
+
+int brr_comm_unique_id(void *out) {
+  if (!out) return -1;
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) { set_error("ncclGetUniqueId: %s", ncclGetErrorString(r)); return -2; }
+  std::memcpy(out, &id, sizeof id);
+  return 0;
+}
+
+int brr_session_comm_init(brr_session *s, const void *unique_id, int32_t nranks, int32_t rank) {
+  if (!s || !unique_id) return -1;
+  if (nranks != s->nshard || rank != s->shard) {
+    set_error("comm (%d ranks, rank %d) does not match the session's shards (%d, %d)", nranks, rank,
+              s->nshard, s->shard);
+    return -1;
+  }
+  HIPCHK(hipSetDevice(s->device));
+  double *e = nullptr, *st = nullptr;
+  if (int rc = brr_session_exchange_buffers(s, &e, &st)) return rc;
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id, sizeof id);
+  ncclResult_t r = ncclCommInitRank(&s->comm, nranks, id, rank);
+  if (r != ncclSuccess) { set_error("ncclCommInitRank: %s", ncclGetErrorString(r)); s->comm = nullptr; return -2; }
+  return 0;
+}
+
+int brr_session_exchange_sizes(brr_session *s, int64_t *n_eps, int64_t *n_stats) {
+  if (!s) return -1;
+  if (n_eps) *n_eps = s->N;
+  if (n_stats) *n_stats = s->NS;
+  return 0;
+}
+
+int brr_session_set_exchange(brr_session *s, double *dev_eps, double *dev_stats) {
+  if (!s) return -1;
+  s->ex_eps = dev_eps;
+  s->ex_stats = dev_stats;
+  return 0;
+}
+
+int brr_session_exchange_buffers(brr_session *s, double **dev_eps, double **dev_stats) {
+  if (!s) return -1;
+  if (!s->ex_eps || !s->ex_stats) {
+    HIPCHK(hipSetDevice(s->device));
+    if (s->alloc(&s->ex_eps, s->N) || s->alloc(&s->ex_stats, s->NS)) return -2;
+    HIPCHK(hipMemset(s->ex_eps, 0, sizeof(double) * s->N));
+    HIPCHK(hipMemset(s->ex_stats, 0, sizeof(double) * s->NS));
+    s->ex_owned = true;
+  }
+  if (dev_eps) *dev_eps = s->ex_eps;
+  if (dev_stats) *dev_stats = s->ex_stats;
+  return 0;
+}
+
+int brr_session_exchange_copy(brr_session *s, int32_t dir, double *host_eps, double *host_stats) {
+  if (!s || !s->ex_eps) { set_error("no exchange buffers"); return -1; }
+  HIPCHK(hipSetDevice(s->device));
+  HIPCHK(hipStreamSynchronize(s->st));
+  const hipMemcpyKind k = dir == 0 ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice;
+  if (host_eps)
+    HIPCHK(dir == 0 ? hipMemcpy(host_eps, s->ex_eps, sizeof(double) * s->N, k)
+                    : hipMemcpy(s->ex_eps, host_eps, sizeof(double) * s->N, k));
+  if (host_stats)
+    HIPCHK(dir == 0 ? hipMemcpy(host_stats, s->ex_stats, sizeof(double) * s->NS, k)
+                    : hipMemcpy(s->ex_stats, host_stats, sizeof(double) * s->NS, k));
+  return 0;
+}
+
+int brr_session_sweep_local(brr_session *s) {
+  if (!s) return -1;
+  HIPCHK(hipSetDevice(s->device));
+  int rc = do_sweep_local(s);
+  if (rc == 0) HIPCHK(hipStreamSynchronize(s->st));  // exchange buffers complete for the caller
+  return rc;
+}
+
+int brr_session_sweep_finish(brr_session *s) {
+  if (!s) return -1;
+  HIPCHK(hipSetDevice(s->device));
+  return do_sweep_finish(s);
+}
+
+int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
+  if (!s || !out) return -1;
+  HIPCHK(hipSetDevice(s->device));
+  if (int rc = ensure_reduced(s)) return rc;
+  Scal sc;
+  if (int rc = d2h(s, &sc, s->d.sc, 1)) return rc;
+  switch (which) {
+    case BRR_MU: *out = sc.mu; return 0;
+    case BRR_SIGMAE: *out = sc.sigmaE; return 0;
+    case BRR_SIGMAF: *out = sc.sigmaF; return 0;
+    case BRR_TAU: *out = sc.tau; return 0;
+    case BRR_ETA: *out = sc.eta; return 0;
+    case BRR_C2: *out = sc.c2; return 0;
+    case BRR_SIGMAG: return d2h(s, out, s->d.sigmaGG, 1);
+    case BRR_SUMSQ_BETA: return d2h(s, out, s->d.stats, 1);
+    default: set_error("unknown scalar %d", which); return -1;
+  }
+}
+
+int brr_session_set_scalar(brr_session *s, int32_t which, double v) {
+  if (!s) return -1;
+  HIPCHK(hipSetDevice(s->device));
+  Scal sc;
+  if (int rc = d2h(s, &sc, s->d.sc, 1)) return rc;
+  switch (which) {
+    case BRR_MU: sc.mu = v; break;
+    case BRR_SIGMAE: sc.sigmaE = v; break;
+    case BRR_SIGMAF: sc.sigmaF = v; break;
+    case BRR_TAU: sc.tau = v; break;
+    case BRR_ETA: sc.eta = v; break;
+    case BRR_C2: sc.c2 = v; break;
+    case BRR_SIGMAG: return h2d(s, s->d.sigmaGG, &v, 1);
+    default: set_error("scalar %d not settable", which); return -1;
+  }
+  s->need_reduce = true;
+  return h2d(s, s->d.sc, &sc, 1);
+}
+
+int64_t brr_session_get_vector(brr_session *s, int32_t which, double *out) {
+  if (!s) return -1;
+  if (hipSetDevice(s->device) != hipSuccess) return -2;
+  int64_t n = -1;
+  switch (which) {
+    case BRR_BETA: case BRR_COMP: case BRR_LAMBDA: case BRR_XSQ: case BRR_ORDER: case BRR_HSV: n = s->M; break;
+    case BRR_EPS: n = s->N; break;
+    case BRR_SIGMAGG: case BRR_BETAACUM: n = s->G; break;
+    case BRR_PI: case BRR_VCOUNT: n = (int64_t)s->G * s->K; break;
+    case BRR_ALPHA: n = s->F; break;
+    default: set_error("unknown vector %d", which); return -1;
+  }
+  if (!out) return n;
+  int rc = 0;
+  switch (which) {
+    case BRR_BETA: rc = d2h(s, out, s->d.beta, n); break;
+    case BRR_EPS: rc = d2h(s, out, s->d.eps, n); break;
+    case BRR_LAMBDA: rc = d2h(s, out, s->d.lambda, n); break;
+    case BRR_HSV: rc = d2h(s, out, s->d.hsv, n); break;
+    case BRR_XSQ: rc = d2h(s, out, s->d.xsq, n); break;
+    case BRR_SIGMAGG: rc = d2h(s, out, s->d.sigmaGG, n); break;
+    case BRR_PI: rc = d2h(s, out, s->d.pi, n); break;
+    case BRR_ALPHA: rc = d2h(s, out, s->d.alpha, n); break;
+    case BRR_BETAACUM: rc = d2h(s, out, s->d.stats + 2, n); break;
+    case BRR_VCOUNT: rc = d2h(s, out, s->d.stats + 2 + s->G, n); break;
+    case BRR_COMP: {
+      std::vector<int> c((size_t)n);
+      rc = d2h(s, c.data(), s->d.comp, n);
+      for (int64_t i = 0; i < n; ++i) out[i] = c[(size_t)i];
+      break;
+    }
+    case BRR_ORDER: {
+      std::vector<int> mem((size_t)s->nb * s->B), bsz((size_t)s->nb);
+      rc = d2h(s, mem.data(), s->d.member, (int64_t)mem.size());
+      rc = rc ? rc : d2h(s, bsz.data(), s->d.bsz, s->nb);
+      int64_t k = 0;
+      for (int b = 0; b < s->nb; ++b)
+        for (int i = 0; i < bsz[(size_t)b]; ++i) out[k++] = (double)(s->col_offset + mem[(size_t)b * s->B + i]);
+      break;
+    }
+  }
+  return rc ? rc : n;
+}
+
+int brr_session_set_vector(brr_session *s, int32_t which, const double *in) {
+  if (!s || !in) return -1;
+  HIPCHK(hipSetDevice(s->device));
+  int rc = 0;
+  switch (which) {
+    case BRR_BETA: rc = h2d(s, s->d.beta, in, s->M); break;
+    case BRR_EPS: rc = h2d(s, s->d.eps, in, s->N); s->need_reduce = true; break;
+    case BRR_LAMBDA: rc = h2d(s, s->d.lambda, in, s->M); break;
+    case BRR_SIGMAGG: rc = h2d(s, s->d.sigmaGG, in, s->G); break;
+    case BRR_PI: rc = h2d(s, s->d.pi, in, (int64_t)s->G * s->K); break;
+    case BRR_ALPHA: rc = h2d(s, s->d.alpha, in, s->F); break;
+    case BRR_COMP: {
+      std::vector<int> c((size_t)s->M);
+      for (int64_t i = 0; i < s->M; ++i) c[(size_t)i] = (int)in[i];
+      rc = h2d(s, s->d.comp, c.data(), s->M);
+      break;
+    }
+    default: set_error("vector %d not settable", which); return -1;
+  }
+  return rc;
+}
+
+int32_t brr_session_iteration(brr_session *s) { return s ? s->iteration : -1; }
+
+int brr_session_set_timing(brr_session *s, int32_t on) {
+  if (!s) return -1;
+  if (int rc = collect_timing(s)) return rc;
+  s->timing = on != 0;
+  if (on) { s->t_stream = s->t_solve = 0; s->n_stream = s->n_solve = 0; }
+  return 0;
+}
+
+int brr_session_timing(brr_session *s, double *stream_ms, int64_t *n_stream, double *solve_ms,
+                       int64_t *n_solve) {
+  if (!s) return -1;
+  if (int rc = collect_timing(s)) return rc;
+  if (stream_ms) *stream_ms = s->t_stream;
+  if (n_stream) *n_stream = s->n_stream;
+  if (solve_ms) *solve_ms = s->t_solve;
+  if (n_solve) *n_solve = s->n_solve;
+  return 0;
+}
+
+int64_t brr_session_block_size(brr_session *s) { return s ? s->B : -1; }
+
+int brr_session_synchronize(brr_session *s) {
+  if (!s) return -1;
+  HIPCHK(hipSetDevice(s->device));
+  HIPCHK(hipStreamSynchronize(s->st));
+  return 0;
+}
+
+}  // extern "C"

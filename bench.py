@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""bench.py -- Gibbs sweeps/s of the MI355X BayesR sampler (BASELINE.json metric).
+
+One step = one full Gibbs sweep (mu, every marker in visit order, hyper-parameters) of
+BayesRSamplerV2 on a synthetic cohort resident in HBM (generated on the device, DESIGN.md
+"synthetic data spec").  Default workload: BASELINE configs[1] (C2), N = 100,000 individuals
+x P = 500,000 f32 genotypes, K = 4 (cva = 1e-4, 1e-3, 1e-2).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5|c1]
+
+For N > 1 the driver launches one process per GPU (torch.distributed.run); markers are
+column-sharded (contiguous blocks) and the residual is kept coherent by one ncclAllReduce per
+sweep inside libbrr (RCCL over xGMI).  torch.distributed is used only with the gloo backend
+for the rendezvous, barriers and the max-over-ranks timing -- torch's own HIP runtime is never
+initialised in the same process as libbrr (they are different ROCm builds).
+Scaling is strong: the same C2 problem is split over the N GPUs.
+
+Prints ONE JSON line on rank 0 (metric/value/unit/..., roofline, cpu_baseline).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "Gibbs sweeps/sec (full SNP pass) at N×P; achieved HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+HYP = dict(sigma0=0.01, v0E=1e-4, s02E=1e-3, v0G=1e-4, s02G=1e-3)  # vignettes/BayesRR.Rmd:93-98
+CVA = [1e-4, 1e-3, 1e-2]
+
+CONFIGS = {
+    "c1": dict(model="v2", N=2_000, P=10_000, groups=1,
+               workload="BayesRSamplerV2 N=2,000 x P=10,000, 3-component mixture (BASELINE configs[0])"),
+    "c2": dict(model="v2", N=100_000, P=500_000, groups=1,
+               workload="BayesRSamplerV2 N=100,000 x P=500,000 dense f32 genotypes, 1 MI355X (BASELINE configs[1])"),
+    "c3": dict(model="groups", N=100_000, P=500_000, groups=22,
+               workload="BayesRSamplerV2Groups N=100,000 x P=500,000, 22 SNP groups (BASELINE configs[2])"),
+    "c4": dict(model="hs", N=100_000, P=500_000, groups=1,
+               workload="HorseshoeR N=100,000 x P=500,000 (BASELINE configs[3])"),
+    "c5": dict(model="v2", N=500_000, P=1_000_000, groups=1,
+               workload="BayesRSamplerV2 N=500,000 x P=1,000,000 column-sharded (BASELINE configs[4])"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--N", type=int, default=None)
+    ap.add_argument("--P", type=int, default=None)
+    ap.add_argument("--block-size", type=int, default=128)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--data-seed", type=int, default=20261015)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-markers", type=int, default=3000,
+                    help="markers in the bounded CPU-baseline sample (N as in the config)")
+    ap.add_argument("--cpu-sweeps", type=int, default=3)
+    ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-roofline-events", action="store_true")
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------------------------------------
+def cpu_baseline_child(args):
+    """Runs in a subprocess pinned to ONE core: the reference-faithful CPU oracle (f64, y~
+    materialised, single thread -- the reference's package build is single-threaded,
+    SURVEY fact 5) on a bounded sample of the same workload."""
+    os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
+    from oracle import oracle as O
+    O.build()
+    cfg = CONFIGS[args.config]
+    N = args.N or cfg["N"]
+    Pm = args.cpu_markers
+    X = O.synth_x(args.data_seed, N, Pm)
+    import numpy as np
+    rng = np.random.default_rng(0)
+    Y = rng.normal(size=N)
+    Y = (Y - Y.mean()) / Y.std(ddof=1)
+    kw = dict(HYP)
+    model = {"v2": O.V2, "groups": O.GROUPS, "hs": O.HORSESHOE}[cfg["model"]]
+    if cfg["model"] == "hs":
+        kw = dict(A=(1 / N ** 0.5) * 1500 / (cfg["P"] - 1500), v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0,
+                  c2=1.0, vC=10.0, sC=10.0)
+    elif cfg["model"] == "groups":
+        import numpy as np
+        G = cfg["groups"]
+        kw.update(G=G, cva=np.tile(CVA, (G, 1)), gAssign=(np.arange(Pm) * G // Pm).astype(np.int32),
+                  fixed=np.zeros((N, 1)))
+    else:
+        kw.update(cva=CVA)
+    o = O.Oracle(model, X, Y, seed=args.seed, order_mode=O.ORDER_REFERENCE, **kw)
+    o.sweep(1)  # warm
+    t0 = time.perf_counter()
+    o.sweep(args.cpu_sweeps)
+    dt = time.perf_counter() - t0
+    print(json.dumps({"t_sweep_sample_s": dt / args.cpu_sweeps, "markers": Pm, "N": N}))
+
+
+def cpu_baseline(args, P_full):
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--config", args.config,
+           "--cpu-markers", str(args.cpu_markers), "--cpu-sweeps", str(args.cpu_sweeps),
+           "--data-seed", str(args.data_seed)]
+    if args.N:
+        cmd += ["--N", str(args.N)]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    if out.returncode != 0:
+        return {"value": None, "unit": "sweeps/s", "cores": 1, "kind": "port",
+                "sample": f"failed: {out.stderr[-300:]}"}
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    t_marker = r["t_sweep_sample_s"] / r["markers"]
+    return {
+        "value": 1.0 / (t_marker * P_full),
+        "unit": "sweeps/s (extrapolated: 1 / (P x t_marker))",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"CPU oracle (reference-faithful C restatement, f64, y~ materialised, 1 thread "
+                   f"pinned) N={r['N']} x {r['markers']} markers, {args.cpu_sweeps} sweeps; "
+                   f"t_marker={t_marker * 1e3:.4f} ms; P={P_full}"),
+        "t_marker_ms": t_marker * 1e3,
+    }
+
+
+# ------------------------------------------------------------------------------------------
+def main():
+    args = parse()
+    if args.cpu_baseline_child:
+        cpu_baseline_child(args)
+        return
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # gloo only: rendezvous / barrier / max-over-ranks
+        dist.init_process_group("gloo")
+    import numpy as np
+    import bayesrrcpp_amd as B
+    from bayesrrcpp_amd import _lib as L
+    from bayesrrcpp_amd.session import comm_unique_id
+
+    cfg = CONFIGS[args.config]
+    N = args.N or cfg["N"]
+    P = args.P or cfg["P"]
+    Bsz = args.block_size
+    model = {"v2": L.MODEL_V2, "groups": L.MODEL_GROUPS, "hs": L.MODEL_HORSESHOE}[cfg["model"]]
+    G = cfg["groups"]
+    # contiguous block shards
+    nb = (P + Bsz - 1) // Bsz
+    b0, b1 = nb * rank // world, nb * (rank + 1) // world
+    c0, c1 = b0 * Bsz, min(P, b1 * Bsz)
+    Pl = c1 - c0
+    K = 1 if model == L.MODEL_HORSESHOE else len(CVA) + 1
+    F = 1 if model == L.MODEL_GROUPS else 0
+    s = B.Session(model, N, Pl, K=K, groups=G, F=F, M_total=P, col_offset=c0, device=local_rank,
+                  block_size=Bsz, order_mode=L.ORDER_BLOCKED, shard_rank=rank, shard_count=world)
+    t_setup = time.perf_counter()
+    s.synthesize(args.data_seed, 0.5, -1)
+    if world > 1:
+        import torch
+        g = torch.from_numpy(s.synth_partial_y())
+        dist.all_reduce(g)
+        s.synth_y(g.numpy(), args.data_seed, 0.5)
+    if model == L.MODEL_HORSESHOE:
+        s.set_horseshoe(A=(1 / N ** 0.5) * 1500 / (P - 1500), v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0,
+                        c2=1.0, vC=10.0, sC=10.0)  # HorseshoeR.cpp:315-323
+    else:
+        gA = (np.arange(c0, c1) * G // P).astype(np.int32) if G > 1 else None
+        s.set_bayesr(cva=np.tile(CVA, (G, 1)), gAssign=gA, **HYP)
+        if F:
+            s.set_fixed(np.zeros((N, F)))  # vignettes/BayesRR.Rmd:166: one all-zero column
+    s.init(args.seed)
+    if world > 1:
+        uid = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        s.comm_init(uid[0], world, rank)
+    s.synchronize()
+    t_setup = time.perf_counter() - t_setup
+
+    def barrier():
+        s.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    s.sweep(args.warmup)
+    barrier()
+    t0 = time.perf_counter()
+    s.sweep(args.steps)
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ms = dt / args.steps * 1e3
+    value = args.steps / dt  # whole-job sweeps/s (every rank holds a shard of the same sweep)
+
+    # roofline of the dominant kernel (k_stream): HIP events around every streaming launch on
+    # the session stream, over a few instrumented sweeps after the timed region
+    roof = None
+    if not args.no_roofline_events:
+        s.set_timing(True)
+        s.sweep(2)
+        tm = s.timing()
+        s.set_timing(False)
+        avg_ms = tm["stream_ms"] / max(1, tm["stream_launches"])
+        bytes_launch = 4.0 * N * Bsz  # algorithmic: one f32 read of the block's B columns
+        achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "k_stream", "avg_launch_us": round(avg_ms * 1e3, 3),
+                "bytes_per_launch": int(bytes_launch),
+                "solve_avg_us": round(tm["solve_ms"] / max(1, tm["solve_launches"]) * 1e3, 3),
+                "sweep_hbm_gbs": round(4.0 * N * Pl / (ms * 1e-3) / 1e9, 1)}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, P)
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 4), "unit": "sweeps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (on-device Binomial(2,f) genotypes, standardised; f32 X, f64 arithmetic)",
+            "config": {"workload": cfg["workload"], "N": N, "P": P, "K": K, "groups": G,
+                       "block_size": Bsz, "order": "blocked", "parallelism": f"column-shard x{world}",
+                       "setup_s": round(t_setup, 2)},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

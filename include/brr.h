@@ -1,0 +1,187 @@
+/*
+ * brr.h -- C ABI of the MI355X BayesR / BayesRR / Horseshoe Gibbs sampler (libbrr.so).
+ *
+ * Drop-in boundary: the four one-shot entry points take exactly the arguments of the
+ * reference's Rcpp-exported C++ functions (plain pointers + sizes instead of Eigen/Rcpp
+ * types) and produce the same output file.  A maintainer binds them from the Rcpp glue
+ * (r_shim/RcppExports.cpp) in place of the reference bodies:
+ *
+ *   brr_BayesRSamplerV2        replaces BayesRSamplerV2        src/BayesRv2.cpp:60
+ *                                       (.Call glue src/RcppExports.cpp:39-59)
+ *   brr_BayesRSamplerV2Groups  replaces BayesRSamplerV2Groups  src/BayesRv2Groups.cpp:75
+ *                                       (.Call glue src/RcppExports.cpp:61-84)
+ *   brr_BRV2Grstart            replaces BRV2Grstart            src/BRv2Grstart.cpp:77
+ *                                       (.Call glue src/RcppExports.cpp:10-37)
+ *   brr_HorseshoeR             replaces HorseshoeR             src/HorseshoeR.cpp:109
+ *                                       (.Call glue src/RcppExports.cpp:86-108)
+ *
+ * Matrices are column-major with leading dimension = rows (R's storage), borrowed and
+ * read-only; the library never copies X on the host (it uploads once, f64 -> f32).
+ *
+ * Return codes: 0 ok; 1 validation abort with the reference's semantics (message through
+ * the log callback, file left as the reference leaves it); < 0 device / IO / argument error
+ * (message through the log callback and brr_last_error()).  No C++ exception crosses the ABI.
+ *
+ * The session API underneath (brr_session_*) is what the one-shot calls, tests and the
+ * benchmark use: device-resident data, explicit sweeps, state read-back and the
+ * column-sharded multi-GPU protocol (one process per GPU, residual exchange once per sweep).
+ */
+#ifndef BRR_H
+#define BRR_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BRR_ABI_VERSION 1
+
+enum brr_model { BRR_MODEL_V2 = 0, BRR_MODEL_GROUPS = 1, BRR_MODEL_RESTART = 2, BRR_MODEL_HORSESHOE = 3 };
+
+/* Visit order of the markers within a sweep.
+ *  BLOCKED   (default) fixed column blocks of size block_size; block order and the order
+ *            inside each block are Philox permutations redrawn every sweep.  Block Gram
+ *            matrices are computed once, so this is the fast path.
+ *  REFERENCE the reference's own order: libstdc++ std::random_shuffle driven by glibc
+ *            rand() from a fresh-process state (BayesRv2.cpp:182), persisting across
+ *            sweeps; Gram blocks are recomputed every sweep (slow; for parity / replay).
+ *  IDENTITY  markers 0..P-1 in index order every sweep (debugging). */
+enum brr_order { BRR_ORDER_BLOCKED = 0, BRR_ORDER_REFERENCE = 1, BRR_ORDER_IDENTITY = 2 };
+
+typedef void (*brr_log_fn)(const char *msg, void *userdata);
+
+typedef struct brr_options {
+  int32_t abi_version;     /* BRR_ABI_VERSION */
+  int32_t device;          /* HIP device ordinal (default 0) */
+  int32_t block_size;      /* marker block B, 64..256, multiple of 64 (default 128) */
+  int32_t order_mode;      /* enum brr_order (default BLOCKED) */
+  int32_t shard_rank;      /* column shard of this process (default 0) */
+  int32_t shard_count;     /* number of column shards / processes (default 1) */
+  int32_t verbose;         /* 1 = progress lines "iteration: i" like the reference */
+  int32_t reserved0;
+  brr_log_fn log;          /* NULL = stderr */
+  void *log_userdata;
+} brr_options;
+
+void brr_options_default(brr_options *opt);
+const char *brr_last_error(void);
+int brr_device_count(void);
+
+/* ---------------- one-shot drop-in entry points (reference signatures) ---------------- */
+int brr_BayesRSamplerV2(const char *outputFile, int seed, int max_iterations, int burn_in,
+                        int thinning, const double *X, int64_t N, int64_t M, const double *Y,
+                        double sigma0, double v0E, double s02E, double v0G, double s02G,
+                        const double *cva, int32_t n_cva, const brr_options *opt);
+
+int brr_BayesRSamplerV2Groups(const char *outputFile, int seed, int max_iterations, int burn_in,
+                              int thinning, const double *X, int64_t N, int64_t M,
+                              const double *Y, double sigma0, double v0E, double s02E,
+                              double v0G, double s02G, const double *cva /* groups x n_cva */,
+                              int32_t n_cva, int groups, const int32_t *gAssign /* M */,
+                              const double *fixed /* N x F */, int64_t F,
+                              const brr_options *opt);
+
+int brr_BRV2Grstart(const char *outputFile, int seed, int max_iterations, int burn_in,
+                    int thinning, double mu, const double *beta /* M */, double sigmaE,
+                    const double *sigmaGG /* groups */, const double *X, int64_t N, int64_t M,
+                    const double *epsilon /* N */, const double *components /* M */,
+                    double sigma0, double v0E, double s02E, double v0G, double s02G,
+                    const double *cva, int32_t n_cva, int groups, const int32_t *gAssign,
+                    const brr_options *opt);
+
+int brr_HorseshoeR(const char *outputFile, int seed, int max_iterations, int burn_in,
+                   int thinning, const double *X, int64_t N, int64_t M, const double *Y,
+                   double A, double v0E, double s02E, double vL, double vT, double c2,
+                   double vC, double sC, const brr_options *opt);
+
+/* ---------------- session API ---------------- */
+typedef struct brr_session brr_session;
+
+/* N rows; M = markers of THIS shard (columns of the X given to upload) ; M_total = all
+ * markers; col_offset = global index of this shard's first marker (multiple of block_size
+ * when shard_count > 1).  K = mixture components incl. zero (n_cva + 1; Horseshoe: 1). */
+brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_total,
+                                int64_t col_offset, int32_t K, int32_t groups, int64_t F,
+                                const brr_options *opt);
+void brr_session_destroy(brr_session *s);
+
+/* X: host column-major N x M (this shard), f64 or f32. */
+int brr_session_upload_x_f64(brr_session *s, const double *X, int64_t ldx);
+int brr_session_upload_x_f32(brr_session *s, const float *X, int64_t ldx);
+/* On-device synthetic cohort (DESIGN.md "synthetic data spec"): standardised Binomial(2,f)
+ * genotypes for this shard's global columns; Y = standardised X beta + noise computed over
+ * all M_total columns' causal set.  Requires shard_count == 1 for Y (else use set_y). */
+int brr_session_synthesize(brr_session *s, uint64_t data_seed, double h2, int64_t n_causal);
+/* sharded synthetic Y: Y = scale(sum over shards of X_c beta_c + noise).  Each process reads
+ * its shard's genetic values, the caller sums them across processes, then every process
+ * calls brr_session_synth_y with the sum (identical Y everywhere). */
+int brr_session_synth_partial_y(brr_session *s, double *out /* N */);
+int brr_session_synth_y(brr_session *s, const double *genetic_sum /* N */, uint64_t data_seed,
+                        double h2);
+int brr_session_set_y(brr_session *s, const double *Y);
+int brr_session_set_fixed(brr_session *s, const double *fixed /* N x F */);
+int brr_session_set_bayesr(brr_session *s, double sigma0, double v0E, double s02E, double v0G,
+                           double s02G, const double *cva /* groups x (K-1) col-major */,
+                           const int32_t *gAssign /* M (this shard) or NULL */);
+int brr_session_set_horseshoe(brr_session *s, double A, double v0E, double s02E, double vL,
+                              double vT, double c2, double vC, double sC);
+/* BRV2Grstart state (src/BRv2Grstart.cpp:77): beta/components for this shard's markers */
+int brr_session_set_restart(brr_session *s, double mu, const double *beta, double sigmaE,
+                            const double *sigmaGG, const double *epsilon,
+                            const double *components);
+/* optional override of the initial mixture proportions pi (groups x K, row-major) */
+int brr_session_set_pi(brr_session *s, const double *pi);
+/* reference init block (draws keyed by seed) + Gram precompute */
+int brr_session_init(brr_session *s, int32_t seed);
+/* n full sweeps on this device (shard_count must be 1, or an exchange callback set) */
+int brr_session_sweep(brr_session *s, int32_t n);
+
+/* column-sharded protocol, one process per GPU:
+ *   brr_session_sweep_local(s)  -> mu, fixed effects, this shard's markers against the
+ *                                  local residual; writes dEps (N doubles) and the partial
+ *                                  statistics into the exchange buffers;
+ *   caller all-reduces (sum) the exchange buffers across processes (RCCL / gloo);
+ *   brr_session_sweep_finish(s) -> eps = eps_start + sum dEps, hyper-parameter draws
+ *                                  (redundant and identical on every process).
+ * Exchange buffers are device memory owned by the caller (e.g. torch tensors), sizes from
+ * brr_session_exchange_sizes(). */
+int brr_session_exchange_sizes(brr_session *s, int64_t *n_eps, int64_t *n_stats);
+int brr_session_set_exchange(brr_session *s, double *dev_eps, double *dev_stats);
+/* session-owned exchange buffers (allocated on first use); host copies for gloo / tests:
+ * dir 0 = device -> host, 1 = host -> device */
+int brr_session_exchange_buffers(brr_session *s, double **dev_eps, double **dev_stats);
+int brr_session_exchange_copy(brr_session *s, int32_t dir, double *host_eps, double *host_stats);
+int brr_session_sweep_local(brr_session *s);
+int brr_session_sweep_finish(brr_session *s);
+
+/* native multi-GPU: RCCL over xGMI, one process per GPU.  Rank 0 creates the 128-byte id,
+ * the caller broadcasts it (MPI, a file, torch.distributed/gloo ...), every rank calls
+ * brr_session_comm_init; brr_session_sweep then runs local sweep -> ncclAllReduce(sum) of
+ * the exchange buffers on the session stream -> finish, with no host round trip. */
+int brr_comm_unique_id(void *out /* 128 bytes */);
+int brr_session_comm_init(brr_session *s, const void *unique_id, int32_t nranks, int32_t rank);
+
+/* state read-back (host buffers) */
+enum brr_scalar { BRR_MU = 0, BRR_SIGMAE, BRR_SIGMAG, BRR_SIGMAF, BRR_TAU, BRR_ETA, BRR_C2,
+                  BRR_SUMSQ_BETA, BRR_N_SCALARS };
+enum brr_vector { BRR_BETA = 0, BRR_COMP, BRR_EPS, BRR_SIGMAGG, BRR_PI, BRR_ALPHA, BRR_LAMBDA,
+                  BRR_XSQ, BRR_ORDER, BRR_VCOUNT, BRR_BETAACUM, BRR_HSV };
+int brr_session_get_scalar(brr_session *s, int32_t which, double *out);
+int64_t brr_session_get_vector(brr_session *s, int32_t which, double *out /* may be NULL */);
+int brr_session_set_vector(brr_session *s, int32_t which, const double *in);
+int brr_session_set_scalar(brr_session *s, int32_t which, double v);
+int32_t brr_session_iteration(brr_session *s);
+
+/* instrumentation: per-launch HIP-event timing of the streaming kernel (dots + residual
+ * update), accumulated over the sweeps run while enabled. */
+int brr_session_set_timing(brr_session *s, int32_t on);
+int brr_session_timing(brr_session *s, double *stream_ms_total, int64_t *stream_launches,
+                       double *solve_ms_total, int64_t *solve_launches);
+/* algorithmic bytes of one streaming launch = 4 * N * block_size */
+int64_t brr_session_block_size(brr_session *s);
+int brr_session_synchronize(brr_session *s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

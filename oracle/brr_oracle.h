@@ -1,0 +1,130 @@
+/*
+ * brr_oracle.h -- CPU restatement of the BayesRRcpp samplers (TEST INFRASTRUCTURE).
+ *
+ * This is the parity oracle. Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it. The product (bayesrrcpp_amd/, libbrr.so) never
+ * includes, links or calls anything under oracle/.
+ *
+ * What it restates (reference = /root/reference, read-only):
+ *   BayesRSamplerV2        src/BayesRv2.cpp:60-294
+ *   BayesRSamplerV2Groups  src/BayesRv2Groups.cpp:75-360
+ *   BRV2Grstart            src/BRv2Grstart.cpp:77-305
+ *   HorseshoeR             src/HorseshoeR.cpp:109-302
+ *   distributions          src/distributions.cpp:12-39,60-62
+ * in double precision, single thread, with y~ materialised per marker exactly
+ * like the reference (three N-length passes per marker), so it doubles as the
+ * reference-faithful CPU timing baseline.
+ *
+ * Two pieces are injected instead of R's global RNG stream:
+ *   - random draws: counter-based Philox4x32-10 keyed by (seed) and counted by
+ *     (slot, tag, entity, iteration) -- see DESIGN.md "RNG spec";
+ *   - visit order: either the reference's own glibc rand() + libstdc++
+ *     std::random_shuffle (ORC_ORDER_REFERENCE, bit-exact with the reference,
+ *     /usr/include/c++/11/bits/stl_algo.h:4568-4582), or the block-restricted
+ *     Philox permutation the GPU fast path uses (ORC_ORDER_BLOCKED), or the
+ *     identity (ORC_ORDER_IDENTITY).
+ *
+ * PARITY STATUS: parity unpinned against the reference's own outputs -- the
+ * reference has no tests, fixtures or golden vectors and
+ * cannot be built here (needs R, Rcpp, RcppEigen and R nmath: SURVEY.md 8c).
+ * Pinned pieces: glibc rand()/random_shuffle visit order (known-answer test
+ * against this container's libc/libstdc++), Philox4x32-10 (Random123 KAT
+ * vectors and rocRAND's implementation), distribution moments (statistical).
+ */
+#ifndef BRR_ORACLE_H
+#define BRR_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORC_V2 = 0, ORC_GROUPS = 1, ORC_RESTART = 2, ORC_HORSESHOE = 3 };
+enum { ORC_ORDER_BLOCKED = 0, ORC_ORDER_REFERENCE = 1, ORC_ORDER_IDENTITY = 2 };
+
+/* RNG tags (counter word y). Must match bayesrrcpp_amd/csrc/brr_rng.hpp. */
+enum {
+  ORC_T_MARKER = 1, ORC_T_MU = 2, ORC_T_SIGMAE = 3, ORC_T_SIGMAG = 4, ORC_T_PI = 5,
+  ORC_T_SIGMAF = 6, ORC_T_FIXED = 7, ORC_T_HS_V = 8, ORC_T_HS_LAMBDA = 9,
+  ORC_T_HS_ETA = 10, ORC_T_HS_TAU = 11, ORC_T_HS_C2 = 12, ORC_T_INIT = 13,
+  ORC_T_PERM_BLOCK = 14, ORC_T_PERM_WITHIN = 15, ORC_T_PERM_FIXED = 16,
+  ORC_T_DATA_FREQ = 32, ORC_T_DATA_GENO = 33, ORC_T_DATA_NOISE = 34
+};
+#define ORC_INIT_IT 0xFFFFFFFFu
+
+typedef struct orc_config {
+  int32_t model;              /* ORC_V2 ... ORC_HORSESHOE */
+  int64_t N, P;               /* individuals, markers */
+  int32_t K;                  /* mixture components incl. the zero one (cva cols + 1) */
+  int32_t G;                  /* groups (V2 / Horseshoe: 1) */
+  int32_t F;                  /* fixed-effect columns (Groups only) */
+  const double *X;            /* N x P, column-major, ld = N */
+  const double *Y;            /* N (V2, Groups, Horseshoe) */
+  const double *fixed;        /* N x F column-major (Groups) */
+  const double *cva;          /* G x (K-1) column-major (V2: 1 x (K-1)) */
+  const int32_t *gAssign;     /* P, 0-based; NULL = all group 0 */
+  double sigma0, v0E, s02E, v0G, s02G;              /* BayesR family */
+  double A, vL, vT, c2, vC, sC;                      /* Horseshoe (v0E,s02E shared) */
+  /* BRV2Grstart inputs (src/BRv2Grstart.cpp:77) */
+  double mu0, sigmaE0;
+  const double *beta0, *sigmaGG0, *eps0, *comp0;
+  int32_t seed;
+  int32_t order_mode;         /* ORC_ORDER_* */
+  int32_t block_size;         /* B for ORC_ORDER_BLOCKED */
+  int32_t n_shards;           /* column shards emulated (1 = single device) */
+  const double *pi0;          /* optional G x K (row-major per group) initial pi override */
+} orc_config;
+
+typedef struct orc orc;
+
+orc *orc_create(const orc_config *cfg);
+void orc_destroy(orc *o);
+/* reference init block: BayesRv2.cpp:146-170 / Groups :170-205 / restart :155-165 / HS :168-195 */
+int orc_init(orc *o);
+/* n full sweeps (one iteration of the reference's `for(iteration...)` loop each) */
+int orc_sweep(orc *o, int n);
+int32_t orc_iteration(const orc *o);
+
+/* state access. names: see orc_get_* in brr_oracle.c */
+enum {
+  ORC_S_MU = 0, ORC_S_SIGMAE, ORC_S_SIGMAG, ORC_S_SIGMAF, ORC_S_TAU, ORC_S_ETA, ORC_S_C2,
+  ORC_S_SUMSQ_BETA, ORC_S_N_SCALARS
+};
+double orc_get_scalar(const orc *o, int which);
+enum {
+  ORC_V_BETA = 0, ORC_V_COMP, ORC_V_EPS, ORC_V_SIGMAGG, ORC_V_PI, ORC_V_ALPHA,
+  ORC_V_LAMBDA, ORC_V_XSQ, ORC_V_ORDER, ORC_V_VCOUNT, ORC_V_BETAACUM, ORC_V_HSV
+};
+int64_t orc_get_vector(const orc *o, int which, double *out); /* returns length; out may be NULL */
+/* overwrite state (for forced-state parity tests) */
+int orc_set_vector(orc *o, int which, const double *in);
+int orc_set_scalar(orc *o, int which, double v);
+
+/* ---- RNG primitives (exported for KAT / cross-implementation tests) ---- */
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+double orc_u53(uint32_t hi, uint32_t lo);
+double orc_uniform(uint64_t seed, uint32_t tag, uint32_t entity, uint32_t it, uint32_t slot);
+double orc_normal(uint64_t seed, uint32_t tag, uint32_t entity, uint32_t it, uint32_t slot);
+double orc_gamma(uint64_t seed, double shape, uint32_t tag, uint32_t entity, uint32_t it);
+/* glibc rand() TYPE_3 emulation seeded with `s` (srand(s)); fills n outputs */
+void orc_glibc_rand(uint32_t s, int n, int32_t *out);
+/* block-restricted permutation (device fast path spec): returns visit order of P markers */
+void orc_blocked_order(uint64_t seed, uint32_t it, int64_t P, int32_t B, int32_t shard,
+                       int64_t col_offset, int32_t *order /* P */);
+
+/* ---- synthetic cohort (DESIGN.md "synthetic data spec") ---- */
+/* Fills X (N x P col-major, doubles holding f32-rounded values) for global columns
+ * [col0, col0+P). Returns 0. */
+int orc_synth_x(uint64_t data_seed, int64_t N, int64_t P, int64_t col0, double *X);
+/* beta_true for global columns [col0, col0+P) out of P_total */
+int orc_synth_beta(uint64_t data_seed, int64_t P_total, int64_t n_causal, int64_t col0,
+                   int64_t P, double *beta_true);
+
+/* ---- reference-faithful one-shot samplers writing the reference CSV ---- */
+int orc_run_csv(const orc_config *cfg, const char *path, int max_iterations, int burn_in,
+                int thinning);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,289 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle on the same seeded
+inputs, the same Philox draws and the same visit order.
+
+Tolerance (BASELINE north_star "within a stated floating-point tolerance"): component
+assignments identical; beta, epsilon, mu, sigmaE, sigmaG, pi, tau, lambda within relative
+1e-9 (f64 on both sides; the only differences are summation order and libm ulps).
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import CVA, HYP
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-9
+
+
+def _cohort(O, N, P, seed=20261015, n_causal=None):
+    X, Y, b = O.synth_cohort(seed, N, P, h2=0.5, n_causal=n_causal)
+    return X, Y, b
+
+
+def _rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    scale = np.maximum(np.abs(b), np.max(np.abs(b)) * 1e-3 + 1e-300)
+    return float(np.max(np.abs(a - b) / scale)) if a.size else 0.0
+
+
+def _compare(sess, orc, O, L, model, tag=""):
+    bg, bo = sess.vector(L.BETA), orc.vector(O.V_BETA)
+    eg, eo = sess.vector(L.EPS), orc.vector(O.V_EPS)
+    assert _rel(bg, bo) < RTOL, f"{tag} beta rel err {_rel(bg, bo)}"
+    assert _rel(eg, eo) < RTOL, f"{tag} eps rel err {_rel(eg, eo)}"
+    assert abs(sess.scalar(L.MU) - orc.scalar(O.S_MU)) <= RTOL * (1 + abs(orc.scalar(O.S_MU))), tag
+    assert _rel([sess.scalar(L.SIGMAE)], [orc.scalar(O.S_SIGMAE)]) < RTOL, tag
+    if model == L.MODEL_HORSESHOE:
+        for a, b in ((L.TAU, O.S_TAU), (L.ETA, O.S_ETA), (L.C2, O.S_C2)):
+            assert _rel([sess.scalar(a)], [orc.scalar(b)]) < RTOL, f"{tag} scalar {a}"
+        assert _rel(sess.vector(L.LAMBDA), orc.vector(O.V_LAMBDA)) < RTOL, tag
+    else:
+        cg, co = sess.vector(L.COMP), orc.vector(O.V_COMP)
+        assert np.array_equal(cg, co), f"{tag} comps differ at {np.nonzero(cg != co)[0][:10]}"
+        assert _rel(sess.vector(L.SIGMAGG), orc.vector(O.V_SIGMAGG)) < RTOL, tag
+        assert _rel(sess.vector(L.PI), orc.vector(O.V_PI)) < RTOL, tag
+        assert np.array_equal(sess.vector(L.VCOUNT), orc.vector(O.V_VCOUNT)), tag
+
+
+def _make(brr, O, model, X, Y, order_mode, B=128, G=1, gAssign=None, fixed=None, cva=CVA,
+          seed=7, restart=None, hs=None):
+    from bayesrrcpp_amd import _lib as L
+    N, P = X.shape
+    K = 1 if model == L.MODEL_HORSESHOE else np.atleast_2d(cva).shape[-1] + 1
+    F = 0 if fixed is None else np.asarray(fixed).reshape(N, -1).shape[1]
+    s = brr.Session(model, N, P, K=K, groups=G, F=F, block_size=B, order_mode=order_mode)
+    s.upload_x(X)
+    okw = {}
+    if model != L.MODEL_RESTART:
+        s.set_y(Y)
+    if model == L.MODEL_HORSESHOE:
+        s.set_horseshoe(**hs)
+        okw.update(hs)
+    else:
+        cva2 = np.tile(np.asarray(cva, float), (G, 1)) if np.ndim(cva) == 1 else np.asarray(cva)
+        s.set_bayesr(HYP["sigma0"], HYP["v0E"], HYP["s02E"], HYP["v0G"], HYP["s02G"], cva2, gAssign)
+        okw.update(HYP)
+        okw.update(cva=cva2, G=G)
+        if gAssign is not None:
+            okw["gAssign"] = gAssign
+    if fixed is not None:
+        s.set_fixed(fixed)
+        okw["fixed"] = fixed
+    if restart is not None:
+        s.set_restart(restart["mu0"], restart["beta0"], restart["sigmaE0"], restart["sigmaGG0"],
+                      restart["eps0"], restart["comp0"])
+        okw.update(restart)
+    s.init(seed)
+    orc = O.Oracle(model, X, None if model == L.MODEL_RESTART else Y, seed=seed,
+                   order_mode=order_mode, block_size=B, N=N, **okw)
+    return s, orc
+
+
+@pytest.mark.parametrize("order", [2, 0, 1])  # IDENTITY, BLOCKED, REFERENCE
+def test_v2_trajectory(brr, oracle_mod, require_gpu, order):
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    X, Y, _ = _cohort(O, 300, 500, n_causal=30)
+    s, orc = _make(brr, O, L.MODEL_V2, X, Y, order)
+    # init state: sigmaE and xsquared
+    assert _rel(s.vector(L.XSQ), orc.vector(O.V_XSQ)) < 1e-12
+    assert _rel([s.scalar(L.SIGMAE)], [orc.scalar(O.S_SIGMAE)]) < 1e-12
+    assert _rel([s.scalar(L.SIGMAG)], [orc.scalar(O.S_SIGMAG)]) == 0.0
+    for it in range(6):
+        s.sweep(1)
+        orc.sweep(1)
+        assert np.array_equal(s.vector(L.ORDER), orc.vector(O.V_ORDER)), f"visit order it={it}"
+        _compare(s, orc, O, L, L.MODEL_V2, tag=f"order={order} it={it}")
+
+
+def test_v2_block64_and_many_sweeps(brr, oracle_mod, require_gpu):
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    X, Y, _ = _cohort(O, 257, 333, n_causal=20)
+    s, orc = _make(brr, O, L.MODEL_V2, X, Y, 0, B=64, cva=[1e-3, 1e-2])
+    for it in range(20):
+        s.sweep(1)
+        orc.sweep(1)
+    _compare(s, orc, O, L, L.MODEL_V2, tag="B=64 20 sweeps")
+
+
+def test_groups_fixed_effects(brr, oracle_mod, require_gpu):
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P, G = 280, 400, 5
+    X, Y, _ = _cohort(O, N, P, n_causal=25)
+    gA = (np.arange(P) * G // P).astype(np.int32)
+    rng = np.random.default_rng(3)
+    fixed = rng.normal(size=(N, 3))
+    cva = np.array([[1e-4, 1e-3, 1e-2]] * G) * (1 + np.arange(G))[:, None]
+    for order in (0, 1):
+        s, orc = _make(brr, O, L.MODEL_GROUPS, X, Y, order, G=G, gAssign=gA, fixed=fixed, cva=cva)
+        for it in range(5):
+            s.sweep(1)
+            orc.sweep(1)
+            _compare(s, orc, O, L, L.MODEL_GROUPS, tag=f"groups order={order} it={it}")
+            assert _rel(s.vector(L.ALPHA), orc.vector(O.V_ALPHA)) < RTOL
+            assert _rel([s.scalar(L.SIGMAF)], [orc.scalar(O.S_SIGMAF)]) < RTOL
+            assert _rel(s.vector(L.BETAACUM), orc.vector(O.V_BETAACUM)) < RTOL
+
+
+def test_restart(brr, oracle_mod, require_gpu):
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P, G = 250, 300, 3
+    X, Y, _ = _cohort(O, N, P, n_causal=20)
+    gA = (np.arange(P) % G).astype(np.int32)
+    # a previous chain's last state (taken from the oracle)
+    prev = O.Oracle(O.GROUPS, X, Y, cva=np.tile(CVA, (G, 1)), G=G, gAssign=gA, seed=3,
+                    order_mode=0, block_size=128, **HYP)
+    prev.sweep(4)
+    st = dict(mu0=prev.scalar(O.S_MU), beta0=prev.vector(O.V_BETA), sigmaE0=prev.scalar(O.S_SIGMAE),
+              sigmaGG0=prev.vector(O.V_SIGMAGG), eps0=prev.vector(O.V_EPS), comp0=prev.vector(O.V_COMP))
+    s, orc = _make(brr, O, L.MODEL_RESTART, X, None, 0, G=G, gAssign=gA, restart=st)
+    assert _rel(s.vector(L.PI), orc.vector(O.V_PI)) < RTOL  # Dirichlet(v+1) from components
+    for it in range(5):
+        s.sweep(1)
+        orc.sweep(1)
+        _compare(s, orc, O, L, L.MODEL_RESTART, tag=f"restart it={it}")
+
+
+@pytest.mark.parametrize("order", [0, 1])
+def test_horseshoe(brr, oracle_mod, require_gpu, order):
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P = 300, 450
+    X, Y, _ = _cohort(O, N, P, n_causal=30)
+    A = (1 / np.sqrt(N)) * 150 / (P - 150)  # HorseshoeR.cpp:317-318 recipe
+    hs = dict(A=A, v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0)
+    s, orc = _make(brr, O, L.MODEL_HORSESHOE, X, Y, order, hs=hs)
+    assert _rel([s.scalar(L.TAU)], [orc.scalar(O.S_TAU)]) < RTOL
+    for it in range(5):
+        s.sweep(1)
+        orc.sweep(1)
+        _compare(s, orc, O, L, L.MODEL_HORSESHOE, tag=f"hs order={order} it={it}")
+
+
+def test_forced_state_single_sweep(brr, oracle_mod, require_gpu):
+    """Identical injected state (beta, comps, pi, sigmas) -> one sweep -> identical result."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    X, Y, _ = _cohort(O, 200, 256, n_causal=20)
+    s, orc = _make(brr, O, L.MODEL_V2, X, Y, 0)
+    rng = np.random.default_rng(11)
+    beta = np.where(rng.random(256) < 0.3, rng.normal(0, 0.05, 256), 0.0)
+    comp = np.where(beta != 0, rng.integers(1, 4, 256), 0).astype(float)
+    pi = np.array([0.6, 0.2, 0.15, 0.05])
+    eps = Y - X @ beta
+    s.set_vector(L.BETA, beta); orc.set_vector(O.V_BETA, beta)
+    s.set_vector(L.COMP, comp); orc.set_vector(O.V_COMP, comp)
+    s.set_vector(L.PI, pi); orc.set_vector(O.V_PI, pi)
+    s.set_vector(L.EPS, eps); orc.set_vector(O.V_EPS, eps)
+    s.set_scalar(L.SIGMAE, 0.6); orc.set_scalar(O.S_SIGMAE, 0.6)
+    s.set_scalar(L.SIGMAG, 0.3); orc.set_scalar(O.S_SIGMAG, 0.3)
+    s.sweep(1)
+    orc.sweep(1)
+    _compare(s, orc, O, L, L.MODEL_V2, tag="forced")
+
+
+def test_synthetic_x_bitwise(brr, oracle_mod, require_gpu):
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P = 777, 100
+    s = brr.Session(L.MODEL_V2, N, P, K=4)
+    s.synthesize(20261015, 0.5, 10)
+    s.set_bayesr(**HYP, cva=CVA)
+    s.init(1)
+    Xo = O.synth_x(20261015, N, P)
+    xsq_o = (Xo * Xo).sum(0)
+    # X identical bit for bit -> identical column norms up to summation order
+    assert _rel(s.vector(L.XSQ), xsq_o) < 1e-12
+    assert np.allclose(s.vector(L.XSQ), N - 1, rtol=1e-5)
+
+
+def test_oneshot_csv_v2(brr, oracle_mod, require_gpu, tmp_path):
+    """The drop-in entry point writes the reference CSV; it matches the oracle's CSV."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    X, Y, _ = _cohort(O, 120, 150, n_causal=10)
+    p_gpu = str(tmp_path / "gpu.csv")
+    p_orc = str(tmp_path / "orc.csv")
+    brr.BayesRSamplerV2(p_gpu, 5, 30, 10, 4, X, Y, HYP["sigma0"], HYP["v0E"], HYP["s02E"],
+                        HYP["v0G"], HYP["s02G"], CVA, log=lambda m: None)
+    O.run_csv(p_orc, O.V2, X, Y, 30, 10, 4, cva=CVA, seed=5, order_mode=0, block_size=128, **HYP)
+    g = open(p_gpu).read().splitlines()
+    o = open(p_orc).read().splitlines()
+    assert g[0] == o[0]  # header
+    assert len(g) == len(o) == 1 + len([i for i in range(10, 30) if i % 4 == 0])
+    for lg, lo in zip(g[1:], o[1:]):
+        a = np.array([float(v) for v in lg.split(", ")])
+        b = np.array([float(v) for v in lo.split(", ")])
+        assert a.shape == b.shape
+        assert np.allclose(a, b, rtol=2e-5, atol=1e-9)
+
+
+def test_oneshot_validation(brr, require_gpu, tmp_path):
+    p = str(tmp_path / "bad.csv")
+    msgs = []
+    X = np.ones((10, 5))
+    brr.BayesRSamplerV2(p, 1, 10, 20, 1, X, np.ones(10), 0.01, 1e-4, 1e-3, 1e-4, 1e-3, CVA,
+                        log=msgs.append)
+    assert any("burn_in has to be a positive integer" in m for m in msgs)
+    assert open(p).read().startswith("iteration,mu,beta[1]")  # header written before the check
+
+
+def test_sharded_two_sessions_match_oracle(brr, oracle_mod, require_gpu):
+    """Column-sharded protocol: two sessions on one GPU, residual deltas and statistics summed
+    on the host (the role ncclAllReduce plays across GPUs) == the oracle's 2-shard emulation."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P, B = 260, 512, 128
+    X, Y, _ = _cohort(O, N, P, n_causal=30)
+    shards = [(0, 256), (256, 256)]
+    sess = []
+    for r, (c0, pl) in enumerate(shards):
+        s = brr.Session(L.MODEL_V2, N, pl, K=4, M_total=P, col_offset=c0, block_size=B,
+                        shard_rank=r, shard_count=2)
+        s.upload_x(X[:, c0:c0 + pl])
+        s.set_y(Y)
+        s.set_bayesr(**HYP, cva=CVA)
+        s.init(9)
+        s.exchange_buffers()
+        sess.append(s)
+    orc = O.Oracle(O.V2, X, Y, cva=CVA, seed=9, order_mode=0, block_size=B, n_shards=2, **HYP)
+    for it in range(4):
+        for s in sess:
+            s.sweep_local()
+        parts = [s.exchange_get() for s in sess]
+        te = parts[0][0] + parts[1][0]
+        ts = parts[0][1] + parts[1][1]
+        for s in sess:
+            s.exchange_set(te, ts)
+            s.sweep_finish()
+        orc.sweep(1)
+        beta = np.concatenate([s.vector(L.BETA) for s in sess])
+        comp = np.concatenate([s.vector(L.COMP) for s in sess])
+        assert np.array_equal(comp, orc.vector(O.V_COMP)), f"it={it}"
+        assert _rel(beta, orc.vector(O.V_BETA)) < RTOL
+        for s in sess:
+            assert _rel(s.vector(L.EPS), orc.vector(O.V_EPS)) < RTOL
+            assert _rel([s.scalar(L.SIGMAE)], [orc.scalar(O.S_SIGMAE)]) < RTOL
+            assert _rel(s.vector(L.PI), orc.vector(O.V_PI)) < RTOL
+
+
+def test_rccl_single_rank(brr, oracle_mod, require_gpu):
+    """brr_session_comm_init + sweep with a 1-rank RCCL communicator runs the native path."""
+    from bayesrrcpp_amd import _lib as L
+    from bayesrrcpp_amd.session import comm_unique_id
+    O = oracle_mod
+    X, Y, _ = _cohort(O, 200, 256, n_causal=20)
+    s = brr.Session(L.MODEL_V2, 200, 256, K=4, shard_rank=0, shard_count=1)
+    s.upload_x(X).set_y(Y).set_bayesr(**HYP, cva=CVA).init(3)
+    s.comm_init(comm_unique_id(), 1, 0)
+    s.sweep(3)
+    orc = O.Oracle(O.V2, X, Y, cva=CVA, seed=3, order_mode=0, block_size=128, **HYP)
+    orc.sweep(3)
+    _compare(s, orc, O, L, L.MODEL_V2, tag="rccl 1 rank")
