@@ -239,10 +239,14 @@ __global__ __launch_bounds__(256) void k_rows(Dev d, int flags, const double *de
   }
   if (flags & ROW_SHIFT) e = (e + d.sc->mu_prev) - d.sc->mu;
   if (flags & ROW_PENDING) {
-    const int np = d.sc->n_pend;
-    for (int p = 0; p < np; ++p) {
-      const double x = valid ? (double)d.X[(int64_t)d.pend_idx[p] * d.ld + row] : 0.0;
-      e = (e + x * d.pend_bo[p]) - x * d.pend_bn[p];
+    const int np = d.sc->n_pend;  // multiple of 8, neutral padding
+    const float *Xr = d.X + (valid ? row : 0);
+    for (int p0 = 0; p0 < np; p0 += 8) {
+      double x[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) x[q] = (double)Xr[(int64_t)d.pend_idx[p0 + q] * d.ld];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) e = (e + x[q] * d.pend_bo[p0 + q]) - x[q] * d.pend_bn[p0 + q];
     }
   }
   if (valid) {
@@ -416,29 +420,34 @@ __global__ __launch_bounds__(256) void k_stream(Dev d, int s) {
   const int rg = blockIdx.x;
   const int64_t row = (int64_t)rg * d.R + t;
   const bool valid = (t < d.R) && (row < d.N);
-  double e = valid ? d.eps[row] : 0.0;
+  // every load is unconditional (clamped row, padded column lists): a per-element
+  // "load or zero" branch makes hipcc wait vmcnt(0) around each load
+  const int64_t rowc = valid ? row : 0;
+  const float *Xr = d.X + rowc;
+  double e = valid ? d.eps[rowc] : 0.0;
   // residual update for the previous block's changed markers: eps = (eps + x b_old) - x b_new
+  // (list padded to a multiple of 8 with b_old = b_new = 0 entries, which leave eps exact)
   const int np = d.sc->n_pend;
   if (np > 0) {
-    for (int p = 0; p < np; ++p) {
-      const double x = valid ? (double)d.X[(int64_t)d.pend_idx[p] * d.ld + row] : 0.0;
-      e = (e + x * d.pend_bo[p]) - x * d.pend_bn[p];
+    for (int p0 = 0; p0 < np; p0 += 8) {
+      double x[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) x[q] = (double)Xr[(int64_t)d.pend_idx[p0 + q] * d.ld];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) e = (e + x[q] * d.pend_bo[p0 + q]) - x[q] * d.pend_bn[p0 + q];
     }
     if (valid) d.eps[row] = e;
   }
-  // partial dots of block position s
+  if (!valid) e = 0.0;
+  // partial dots of block position s (member list padded with column 0 beyond bs)
   const int bs = d.bsz[s];
   const int *mem = d.member + (int64_t)s * d.B;
-  const float *Xr = d.X + row;
   for (int c0 = 0; c0 < bs; c0 += 32) {
     double v[32];
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const int c = c0 + j;
-      float x = 0.f;
-      if (c < bs && valid) x = Xr[(int64_t)mem[c] * d.ld];
-      v[j] = (double)x * e;
-    }
+    for (int j = 0; j < 32; ++j) v[j] = (double)Xr[(int64_t)mem[c0 + j] * d.ld];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] *= e;
     const double r = wave_reduce32(v, lane);
     if ((lane & 1) == 0) part[w][reduce32_col(lane)] = r;
     __syncthreads();
@@ -544,11 +553,10 @@ __device__ Decision decide_bayesr(double num, double xsq, double sigmaE, double 
 
 // ------------------------------------------------------------------------------------
 // k_solve: one workgroup.  Exact single-site updates of block position s in visit order.
-template <bool HS>
+template <bool HS, int B>
 __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int B = d.B;
   double *Gl = reinterpret_cast<double *>(smem);           // B*B
   double *r_ = Gl + (int64_t)B * B;                           // B each:
   double *tlo = r_ + B, *thi = tlo + B, *den = thi + B, *sdz = den + B, *bold = sdz + B,
@@ -561,10 +569,14 @@ __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it) {
   const int gb = d.gblk[s];
   // 1) Gram block -> LDS (row-major, stride B)
   {
-    const double2 *src = reinterpret_cast<const double2 *>(d.gram + (int64_t)gb * B * B);
-    double2 *dst = reinterpret_cast<double2 *>(Gl);
-    const int n2 = B * B / 2;
-    for (int q = t; q < n2; q += 256) dst[q] = src[q];
+    const double2 *src = reinterpret_cast<const double2 *>(d.gram + (int64_t)gb * B * B) + t;
+    double2 *dst = reinterpret_cast<double2 *>(Gl) + t;
+    constexpr int NQ = B * B / 2 / 256;
+    double2 tmp[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) tmp[q] = src[q * 256];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) dst[q * 256] = tmp[q];
   }
   // 2) per-marker preparation, one thread per position
   const Scal sc = *d.sc;
@@ -572,7 +584,13 @@ __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it) {
     const int m = d.member[(int64_t)s * B + t];
     const int64_t gm = d.col_offset + m;
     double dsum = 0.0;
-    for (int q = 0; q < d.NG; ++q) dsum += d.slab2[(int64_t)q * B + t];
+    for (int q0 = 0; q0 < d.NG; q0 += 8) {  // slab2 rows padded to a multiple of 8 (zeros)
+      double v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = d.slab2[(int64_t)(q0 + q) * B + t];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) dsum += v[q];
+    }
     const double bo = d.beta[m];
     const double x2 = d.xsq[m];
     const double r = dsum + x2 * bo;  // num = x.(eps + x b_old)
@@ -610,7 +628,7 @@ __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it) {
   // 3) serial chain on wave 0: lane l owns positions l and l + 64
   if (t < 64) {
     const int lane = t;
-    constexpr int NS = BMAX / 64;
+    constexpr int NS = B / 64;
     double r[NS], lo[NS], hi[NS], dn[NS], sz[NS], bo[NS];
     int kk[NS], gg[NS];
 #pragma unroll
@@ -727,7 +745,14 @@ __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it) {
     d.pend_bo[idx] = bold[t];
     d.pend_bn[idx] = bnw[t];
   }
-  if (t == 0) d.sc->n_pend = misc[0] + misc[1] + misc[2] + misc[3];
+  const int npend = misc[0] + misc[1] + misc[2] + misc[3];
+  const int npad = (npend + 7) & ~7;
+  if (t >= npend && t < npad) {  // neutral padding: eps + x*0 - x*0 == eps exactly
+    d.pend_idx[t] = 0;
+    d.pend_bo[t] = 0.0;
+    d.pend_bn[t] = 0.0;
+  }
+  if (t == 0) d.sc->n_pend = npad;
 }
 
 // ------------------------------------------------------------------------------------
@@ -965,18 +990,29 @@ size_t solve_lds_bytes(int B) { return (size_t)B * B * 8 + (size_t)B * 9 * 8 + (
 
 hipError_t launch_solve(const Dev &d, int s, uint32_t it, hipStream_t st) {
   const size_t lds = solve_lds_bytes(d.B);
-  if (d.model == MODEL_HORSESHOE)
-    hipLaunchKernelGGL(k_solve<true>, dim3(1), dim3(256), lds, st, d, s, it);
-  else
-    hipLaunchKernelGGL(k_solve<false>, dim3(1), dim3(256), lds, st, d, s, it);
+  const bool hs = d.model == MODEL_HORSESHOE;
+  if (d.B == 64) {
+    if (hs) hipLaunchKernelGGL((k_solve<true, 64>), dim3(1), dim3(256), lds, st, d, s, it);
+    else hipLaunchKernelGGL((k_solve<false, 64>), dim3(1), dim3(256), lds, st, d, s, it);
+  } else {
+    if (hs) hipLaunchKernelGGL((k_solve<true, 128>), dim3(1), dim3(256), lds, st, d, s, it);
+    else hipLaunchKernelGGL((k_solve<false, 128>), dim3(1), dim3(256), lds, st, d, s, it);
+  }
   return hipGetLastError();
 }
 
-hipError_t set_solve_lds_limit(int B) {
-  const int lds = (int)solve_lds_bytes(B);
-  hipError_t e = hipFuncSetAttribute((const void *)k_solve<true>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void *)k_solve<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+hipError_t set_solve_lds_limit(int /*B*/) {
+  // One limit for every variant, the largest any block size needs: lowering it for one
+  // session silently shrank the LDS window of later launches (out-of-range LDS writes are
+  // dropped, no fault).
+  const int lds = (int)solve_lds_bytes(BMAX);
+  const void *fns[4] = {(const void *)k_solve<true, 64>, (const void *)k_solve<false, 64>,
+                        (const void *)k_solve<true, 128>, (const void *)k_solve<false, 128>};
+  for (const void *f : fns) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_markers(const Dev &d, int mode, uint32_t it, hipStream_t st) {

@@ -382,6 +382,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   d.R = (int)std::min<int64_t>(256, std::max<int64_t>(1, (N + target - 1) / target));
   d.RG = (int)((N + d.R - 1) / d.R);
   d.NG = (d.RG + STREAM_GROUP - 1) / STREAM_GROUP;
+  const int NGpad = (d.NG + 7) / 8 * 8;  // k_solve reads slab2 in unconditional batches of 8
   d.MRG = (int)((M + 255) / 256);
   const int64_t RGrows = (N + 255) / 256;
   int rc = 0;
@@ -408,7 +409,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   rc |= s->alloc(&d.gblk, s->nb);
   rc |= s->alloc(&d.blkorder, s->nb);
   rc |= s->alloc(&d.slab1, (int64_t)d.RG * B);
-  rc |= s->alloc(&d.slab2, (int64_t)d.NG * B);
+  rc |= s->alloc(&d.slab2, (int64_t)NGpad * B);
   rc |= s->alloc(&d.cnt1, d.NG);
   rc |= s->alloc(&d.pend_idx, B);
   rc |= s->alloc(&d.pend_bo, B);
@@ -422,7 +423,15 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   d.deps = nullptr;
   if (rc) { delete s; return nullptr; }
   d.gAssign = nullptr;
+  // every buffer a kernel may read before writing is zeroed here (recycled device memory
+  // holds the previous session's values): slab2 pad rows, member padding, pending list
   bool ok = hipMemsetAsync(d.cnt1, 0, sizeof(int) * d.NG, s->st) == hipSuccess &&
+            hipMemsetAsync(d.slab2, 0, sizeof(double) * NGpad * B, s->st) == hipSuccess &&
+            hipMemsetAsync(d.member, 0, sizeof(int) * s->nb * B, s->st) == hipSuccess &&
+            hipMemsetAsync(d.gidx, 0, sizeof(int) * s->nb * B, s->st) == hipSuccess &&
+            hipMemsetAsync(d.pend_idx, 0, sizeof(int) * B, s->st) == hipSuccess &&
+            hipMemsetAsync(d.pend_bo, 0, sizeof(double) * B, s->st) == hipSuccess &&
+            hipMemsetAsync(d.pend_bn, 0, sizeof(double) * B, s->st) == hipSuccess &&
             hipMemsetAsync(d.rcnt, 0, sizeof(int), s->st) == hipSuccess &&
             hipMemsetAsync(d.mcnt, 0, sizeof(int), s->st) == hipSuccess &&
             hipMemsetAsync(d.sc, 0, sizeof(Scal), s->st) == hipSuccess &&

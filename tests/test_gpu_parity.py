@@ -287,3 +287,22 @@ def test_rccl_single_rank(brr, oracle_mod, require_gpu):
     orc = O.Oracle(O.V2, X, Y, cva=CVA, seed=3, order_mode=0, block_size=128, **HYP)
     orc.sweep(3)
     _compare(s, orc, O, L, L.MODEL_V2, tag="rccl 1 rank")
+
+
+def test_recycled_device_memory(brr, oracle_mod, require_gpu):
+    """Sessions of different shapes back to back: a later session gets the earlier one's
+    freed device memory and must not read any of it before writing (regression: slab2 pad
+    rows / member padding were once left uninitialised)."""
+    import gc
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    for (N, P, B, cva) in [(257, 333, 64, [1e-3, 1e-2]), (257, 333, 128, [1e-3, 1e-2]),
+                           (600, 333, 64, [1e-3, 1e-2]), (257, 333, 64, list(CVA))]:
+        X, Y, _ = _cohort(O, N, P, n_causal=20)
+        s, orc = _make(brr, O, L.MODEL_V2, X, Y, 0, B=B, cva=cva)
+        for it in range(3):
+            s.sweep(1)
+            orc.sweep(1)
+        _compare(s, orc, O, L, L.MODEL_V2, tag=f"recycled N={N} B={B}")
+        del s, orc
+        gc.collect()
