@@ -28,6 +28,8 @@ struct Scal {
   double S2;   // ||eps||^2        (BayesRv2.cpp:251 operand)
   int n_pend;  // pending residual updates (previous block's changed markers)
   int pad;
+  unsigned long long n_slow;     // diagnostics: serial steps that needed the exact re-evaluation
+  unsigned long long n_changed;  // diagnostics: markers whose beta changed
 };
 
 struct Hyper {

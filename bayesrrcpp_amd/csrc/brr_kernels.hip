@@ -77,6 +77,29 @@ __device__ __forceinline__ bool last_arriver(int *cnt, int total, int *lds_flag)
   return *lds_flag != 0;
 }
 
+// Write-through variant (MI355X_MICROARCH.md "Valid forms", row 1): every payload byte stored
+// sc1 (8-B agent-scope relaxed atomic stores) and drained by every storing wave, one relaxed
+// agent add per workgroup; the last arriver reads the payload with sc1 loads only -- no
+// release / acquire fences (no L2 write-back, no L1 invalidate).
+__device__ __forceinline__ void st_sc1(double *p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), __double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double *p) {
+  return __longlong_as_double(__hip_atomic_load(reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ bool last_arriver_wt(int *cnt, int total, int *lds_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *lds_flag = (old == total - 1);
+  }
+  __syncthreads();
+  return *lds_flag != 0;
+}
+
 // ------------------------------------------------------------------------------------
 // Synthetic cohort (DESIGN.md "synthetic data spec"; mirrored by oracle orc_synth_x).
 __device__ __forceinline__ int genotype(uint64_t ds, int64_t i, int64_t j, uint32_t att, double t0,
@@ -301,10 +324,21 @@ __device__ void fisher_yates_dev(uint64_t seed, int *a, int n, uint32_t tag, uin
   }
 }
 
-__global__ void k_perm_blockorder(Dev d, uint32_t it, int shard) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  for (int b = 0; b < d.nb; ++b) d.blkorder[b] = b;
-  fisher_yates_dev(d.seed, d.blkorder, d.nb, T_PERM_BLOCK, (uint32_t)shard, it);
+// Block order: Fisher-Yates in LDS (serial by definition), then one coalesced write.
+constexpr int PERM_LDS_MAX = 32768;  // blocks per shard handled in LDS (128 KiB)
+__global__ __launch_bounds__(256) void k_perm_blockorder(Dev d, uint32_t it, int shard) {
+  extern __shared__ __attribute__((aligned(16))) int ord[];
+  const int nb = d.nb;
+  if (nb <= PERM_LDS_MAX) {
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) ord[b] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) fisher_yates_dev(d.seed, ord, nb, T_PERM_BLOCK, (uint32_t)shard, it);
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) d.blkorder[b] = ord[b];
+  } else if (threadIdx.x == 0) {
+    for (int b = 0; b < nb; ++b) d.blkorder[b] = b;
+    fisher_yates_dev(d.seed, d.blkorder, nb, T_PERM_BLOCK, (uint32_t)shard, it);
+  }
 }
 
 __global__ void k_perm_within(Dev d, uint32_t it, int identity) {
@@ -411,59 +445,81 @@ __device__ __forceinline__ int reduce32_col(int lane) {
          ((lane >> 2) & 1) * 2 + ((lane >> 1) & 1);
 }
 
-__global__ __launch_bounds__(256) void k_stream(Dev d, int s) {
+// Geometry: workgroup rg owns rows [rg*R, rg*R + R), R <= 256 a multiple of 4; lane l owns the
+// 4 consecutive rows rg*R + 4l .. +3 (one 16-B load per column), wave w owns the B/4 columns
+// [w B/4, (w+1) B/4) of the block.  X and eps are padded to ld rows (zeros), so every load is
+// unconditional.  The residual update is applied redundantly by the 4 waves (the re-read
+// columns hit the CU's L1/L2) and written back by wave 0: no barrier in the streaming part.
+template <int B>
+__global__ __launch_bounds__(256, 2) void k_stream(Dev d, int s) {
 #pragma clang fp contract(off)
-  __shared__ double part[4][32];
+  constexpr int CW = B / 4;  // columns per wave (<= 32)
   __shared__ int s_last;
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6;
   const int rg = blockIdx.x;
-  const int64_t row = (int64_t)rg * d.R + t;
-  const bool valid = (t < d.R) && (row < d.N);
-  // every load is unconditional (clamped row, padded column lists): a per-element
-  // "load or zero" branch makes hipcc wait vmcnt(0) around each load
-  const int64_t rowc = valid ? row : 0;
+  const int64_t row0 = (int64_t)rg * d.R + 4 * lane;
+  const bool valid = 4 * lane < d.R && row0 < d.N;
+  const int64_t rowc = valid ? row0 : 0;
   const float *Xr = d.X + rowc;
-  double e = valid ? d.eps[rowc] : 0.0;
-  // residual update for the previous block's changed markers: eps = (eps + x b_old) - x b_new
-  // (list padded to a multiple of 8 with b_old = b_new = 0 entries, which leave eps exact)
+  const int64_t ld = d.ld;
+  // block columns first: their loads do not depend on the residual update
+  const int *mem = d.member + (int64_t)s * B + w * CW;
+  float4 x[CW];
+#pragma unroll
+  for (int j = 0; j < CW; ++j) x[j] = *reinterpret_cast<const float4 *>(Xr + (int64_t)mem[j] * ld);
+  const double2 ea = *reinterpret_cast<const double2 *>(d.eps + rowc);
+  const double2 eb = *reinterpret_cast<const double2 *>(d.eps + rowc + 2);
+  double e0 = ea.x, e1 = ea.y, e2 = eb.x, e3 = eb.y;
+  // residual update for the previous block's changed markers, eps = (eps + x b_old) - x b_new
+  // (BayesRv2.cpp:191,243); list padded to a multiple of 32 with neutral b_old = b_new = 0
   const int np = d.sc->n_pend;
-  if (np > 0) {
-    for (int p0 = 0; p0 < np; p0 += 8) {
-      double x[8];
+  for (int p0 = 0; p0 < np; p0 += 16) {
+    float4 xp[16];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) x[q] = (double)Xr[(int64_t)d.pend_idx[p0 + q] * d.ld];
+    for (int q = 0; q < 16; ++q) xp[q] = *reinterpret_cast<const float4 *>(Xr + (int64_t)d.pend_idx[p0 + q] * ld);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) e = (e + x[q] * d.pend_bo[p0 + q]) - x[q] * d.pend_bn[p0 + q];
+    for (int q = 0; q < 16; ++q) {
+      const double bo = d.pend_bo[p0 + q], bn = d.pend_bn[p0 + q];
+      const double a0 = xp[q].x, a1 = xp[q].y, a2 = xp[q].z, a3 = xp[q].w;
+      e0 = (e0 + a0 * bo) - a0 * bn;
+      e1 = (e1 + a1 * bo) - a1 * bn;
+      e2 = (e2 + a2 * bo) - a2 * bn;
+      e3 = (e3 + a3 * bo) - a3 * bn;
     }
-    if (valid) d.eps[row] = e;
   }
-  if (!valid) e = 0.0;
-  // partial dots of block position s (member list padded with column 0 beyond bs)
-  const int bs = d.bsz[s];
-  const int *mem = d.member + (int64_t)s * d.B;
-  for (int c0 = 0; c0 < bs; c0 += 32) {
-    double v[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) v[j] = (double)Xr[(int64_t)mem[c0 + j] * d.ld];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) v[j] *= e;
-    const double r = wave_reduce32(v, lane);
-    if ((lane & 1) == 0) part[w][reduce32_col(lane)] = r;
-    __syncthreads();
-    if (t < 32 && c0 + t < bs)
-      d.slab1[(int64_t)rg * d.B + c0 + t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
-    __syncthreads();
+  if (np > 0 && w == 0 && valid) {
+    *reinterpret_cast<double2 *>(d.eps + row0) = make_double2(e0, e1);
+    *reinterpret_cast<double2 *>(d.eps + row0 + 2) = make_double2(e2, e3);
   }
+  if (!valid) e0 = e1 = e2 = e3 = 0.0;
+  // partial dots: 4 rows per lane, then the wave transpose-reduction over the 64 lanes
+  double v[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    if (j < CW) {
+      v[j] = (((double)x[j].x * e0 + (double)x[j].y * e1) + (double)x[j].z * e2) + (double)x[j].w * e3;
+    } else {
+      v[j] = 0.0;
+    }
+  }
+  const double r = wave_reduce32(v, lane);
+  const int col = reduce32_col(lane);
+  if ((lane & 1) == 0 && col < CW) st_sc1(d.slab1 + (int64_t)rg * B + w * CW + col, r);
   // level-2: last arriver of the group sums the group's partials in workgroup order
+  const int bs = d.bsz[s];
   const int grp = rg / STREAM_GROUP;
   const int g0 = grp * STREAM_GROUP;
   const int gsz = min(STREAM_GROUP, d.RG - g0);
-  if (last_arriver(d.cnt1 + grp, gsz, &s_last)) {
-    for (int c = t; c < bs; c += 256) {
+  if (last_arriver_wt(d.cnt1 + grp, gsz, &s_last)) {
+    if (t < bs) {
+      double v16[STREAM_GROUP];
+#pragma unroll
+      for (int q = 0; q < STREAM_GROUP; ++q) v16[q] = q < gsz ? ld_sc1(d.slab1 + (int64_t)(g0 + q) * B + t) : 0.0;
       double acc = 0.0;
-      for (int q = 0; q < gsz; ++q) acc += d.slab1[(int64_t)(g0 + q) * d.B + c];
-      d.slab2[(int64_t)grp * d.B + c] = acc;
+#pragma unroll
+      for (int q = 0; q < STREAM_GROUP; ++q) acc += v16[q];
+      d.slab2[(int64_t)grp * B + t] = acc;
     }
     if (t == 0) d.cnt1[grp] = 0;
   }
@@ -538,36 +594,67 @@ __device__ Decision decide_bayesr(double num, double xsq, double sigmaE, double 
   r.denom = (sel != FALLTHROUGH && sel > 0) ? denom[sel - 1] : 1.0;
   r.margin = 0.0;
   if (want_margin && smax > 0.0) {
-    // |d A_k / dt| <= max_k slope_k (softmax derivative bound), see DESIGN.md
-    double gap;
+    // Decision-invariant window in t = num^2 (DESIGN.md "decision margins").  Without active
+    // guards A_k(t) = sum_{j<=k} P_j(t) with P = softmax(logL), logL_j = a_j + b_j t, so
+    //   dA_k/dt = A_k (1 - A_k) (bbar_{<=k} - bbar_{>k}),  |.| <= min(A_k, 1-A_k) b_max,
+    // and over |t - t0| <= delta <= 1/b_max both A_k and 1-A_k grow by at most e^{b_max delta}
+    // <= e.  So A_k stays on its side of p while delta <= gap / (e b_max min(A_k, 1-A_k)).
+    bool any_guard = false;
+    for (int kk = 0; kk < K; ++kk)
+      for (int i = 1; i < K; ++i) any_guard |= fabs(logL[i] - logL[kk]) > 700.0;
+    const double E = 2.718281828459045;
+    auto side = [&](double gap, double Ak) -> double {
+      if (!(gap > 1e-12)) return 0.0;
+      if (any_guard) return gap / smax;
+      const double m = fmin(Ak, 1.0 - Ak);
+      return m > 0.0 ? gap / (E * smax * m) : 1e300;
+    };
+    double w;
     if (sel == FALLTHROUGH) {
-      gap = p - A[K - 1];
+      w = side(p - A[K - 1], A[K - 1]);
     } else {
-      gap = A[sel] - p;
-      if (sel > 0) gap = fmin(gap, p - A[sel - 1]);
+      w = side(A[sel] - p, A[sel]);
+      if (sel > 0) w = fmin(w, side(p - A[sel - 1], A[sel - 1]));
     }
-    if (gap > 1e-12) r.margin = 0.5 * fmin(gap / smax, gmargin);
+    w = fmin(w, 1.0 / smax);
+    r.margin = 0.5 * fmin(w, gmargin);
   }
   return r;
 }
 
 // ------------------------------------------------------------------------------------
 // k_solve: one workgroup.  Exact single-site updates of block position s in visit order.
+// Slow path of the serial chain: exact re-evaluation (reference formula) of position i with
+// its corrected dot product, when the corrected num^2 left the decision-invariant interval.
+__device__ __forceinline__ int chain_slow(const Dev &d, double num, double x2, int g,
+                                                    double p, double z, double sigmaE,
+                                                    double *bnew, double bold) {
+  Decision dc = decide_bayesr(num, x2, sigmaE, d.sigmaGG[g], d.pi + (int64_t)g * d.K, d.cva + g, d.G,
+                              d.K, p, false);
+  *bnew = dc.k == 0 ? 0.0 : (dc.k == FALLTHROUGH ? bold : num / dc.denom + sqrt(sigmaE / dc.denom) * z);
+  return dc.k;
+}
+
 template <bool HS, int B>
 __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it) {
 #pragma clang fp contract(off)
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  double *Gl = reinterpret_cast<double *>(smem);           // B*B
-  double *r_ = Gl + (int64_t)B * B;                           // B each:
-  double *tlo = r_ + B, *thi = tlo + B, *den = thi + B, *sdz = den + B, *bold = sdz + B,
-         *bnw = bold + B, *pp = bnw + B, *xq = pp + B;
-  int *k0 = reinterpret_cast<int *>(xq + B);
+  double *Gl = reinterpret_cast<double *>(smem);  // B*B
+  double *r_ = Gl + (int64_t)B * B;                 // B each:
+  double *tlo = r_ + B, *thi = tlo + B, *ide = thi + B, *sdz = ide + B, *bold = sdz + B,
+         *bnw = bold + B, *pz = bnw + B, *xq = pz + B, *pu = xq + B;
+  int *k0 = reinterpret_cast<int *>(pu + B);
   int *gi = k0 + B, *grp = gi + B, *ksel = grp + B, *mrk = ksel + B, *misc = mrk + B;
 
   const int t = threadIdx.x;
   const int bs = d.bsz[s];
   const int gb = d.gblk[s];
-  // 1) Gram block -> LDS (row-major, stride B)
+  // 1) Gram block -> LDS (row-major, stride B), overlapped with the first batch of the
+  //    dot-product reduction loads (slab2 rows padded to a multiple of 32 with zeros)
+  const int tc = t < B ? t : 0;
+  double sv[32];
+#pragma unroll
+  for (int q = 0; q < 32; ++q) sv[q] = d.slab2[(int64_t)q * B + tc];
   {
     const double2 *src = reinterpret_cast<const double2 *>(d.gram + (int64_t)gb * B * B) + t;
     double2 *dst = reinterpret_cast<double2 *>(Gl) + t;
@@ -578,19 +665,20 @@ __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) dst[q * 256] = tmp[q];
   }
+  double dsum = 0.0;
+#pragma unroll
+  for (int q = 0; q < 32; ++q) dsum += sv[q];
+  for (int q0 = 32; q0 < d.NG; q0 += 32) {
+#pragma unroll
+    for (int q = 0; q < 32; ++q) sv[q] = d.slab2[(int64_t)(q0 + q) * B + tc];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) dsum += sv[q];
+  }
   // 2) per-marker preparation, one thread per position
   const Scal sc = *d.sc;
   if (t < bs) {
     const int m = d.member[(int64_t)s * B + t];
     const int64_t gm = d.col_offset + m;
-    double dsum = 0.0;
-    for (int q0 = 0; q0 < d.NG; q0 += 8) {  // slab2 rows padded to a multiple of 8 (zeros)
-      double v[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = d.slab2[(int64_t)(q0 + q) * B + t];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) dsum += v[q];
-    }
     const double bo = d.beta[m];
     const double x2 = d.xsq[m];
     const double r = dsum + x2 * bo;  // num = x.(eps + x b_old)
@@ -602,35 +690,39 @@ __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it) {
     grp[t] = g;
     bold[t] = bo;
     xq[t] = x2;
-    pp[t] = z;  // the normal draw; the slow path re-derives p from its counter
+    pz[t] = z;
+    pu[t] = p;
     r_[t] = r;
     if (HS) {
       const double lam = d.lambda[m];
       const double sv = sc.tau * sc.c2 * lam / (sc.tau * lam + sc.c2);
       const double D = x2 + (sc.sigmaE / sv);
-      den[t] = D;
-      sdz[t] = sqrt(sc.sigmaE / D) * z;
+      ide[t] = 1.0 / D;
+      sdz[t] = sqrt(sc.sigmaE / D) * z;  // HorseshoeR.cpp:234
       k0[t] = 1;
       tlo[t] = 0.0;
-      thi[t] = -1.0;
+      thi[t] = 1e308;
     } else {
       Decision dc = decide_bayesr(r, x2, sc.sigmaE, d.sigmaGG[g], d.pi + (int64_t)g * d.K,
                                   d.cva + g, d.G, d.K, p, true);
       k0[t] = dc.k;
-      den[t] = dc.denom;
-      sdz[t] = sqrt(sc.sigmaE / dc.denom) * z;
+      ide[t] = 1.0 / dc.denom;
+      sdz[t] = sqrt(sc.sigmaE / dc.denom) * z;  // BayesRv2.cpp:228
       const double t0 = r * r;
       tlo[t] = t0 - dc.margin;
       thi[t] = dc.margin > 0.0 ? t0 + dc.margin : -1.0;  // empty interval -> slow path
     }
   }
   __syncthreads();
-  // 3) serial chain on wave 0: lane l owns positions l and l + 64
+  // 3) serial chain on wave 0 (lane l owns positions l + 64 q).  A ballot finds the next
+  //    position whose update may change beta (fast decision changes it, or its corrected num^2
+  //    left the invariant window); runs of unchanged positions are committed in one step.  The
+  //    owner's new beta is broadcast by readlane and every later position subtracts G_ji*delta.
   if (t < 64) {
     const int lane = t;
     constexpr int NS = B / 64;
-    double r[NS], lo[NS], hi[NS], dn[NS], sz[NS], bo[NS];
-    int kk[NS], gg[NS];
+    double r[NS], lo[NS], hi[NS], id[NS], sz[NS], bo[NS], bf[NS];
+    int kk[NS], gg[NS], kf[NS];
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
       const int pos = q * 64 + lane;
@@ -638,87 +730,70 @@ __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it) {
       r[q] = in ? r_[pos] : 0.0;
       lo[q] = in ? tlo[pos] : 0.0;
       hi[q] = in ? thi[pos] : -1.0;
-      dn[q] = in ? den[pos] : 1.0;
+      id[q] = in ? ide[pos] : 0.0;
       sz[q] = in ? sdz[pos] : 0.0;
       bo[q] = in ? bold[pos] : 0.0;
       kk[q] = in ? k0[pos] : 0;
       gg[q] = in ? gi[pos] : 0;
+      bf[q] = bo[q];
+      kf[q] = kk[q];
     }
+    int nslow = 0;
     int i = 0;
     while (i < bs) {
-      // speculative scan: first position >= i whose update may change beta
-      uint64_t bal[NS];
+      int first = bs;
 #pragma unroll
-      for (int q = 0; q < NS; ++q) {
+      for (int q = NS - 1; q >= 0; --q) {
         const int pos = q * 64 + lane;
         const double tt = r[q] * r[q];
         const bool fast = tt >= lo[q] && tt <= hi[q];
-        const bool nochange = fast && (kk[q] == FALLTHROUGH || (kk[q] == 0 && bo[q] == 0.0));
-        bal[q] = __ballot(pos >= i && pos < bs && (HS || !nochange));
+        const bool nochange = !HS && fast && (kk[q] == FALLTHROUGH || (kk[q] == 0 && bo[q] == 0.0));
+        const uint64_t bal = __ballot(pos >= i && pos < bs && !nochange);
+        if (bal) first = q * 64 + __builtin_ctzll(bal);
       }
-      int first = bs;
+      if (first >= bs) break;  // the rest keep their fast decisions (no change)
+      const int qs = first >> 6, l = first & 63;  // wave-uniform
+      double rv = r[0], lov = lo[0], hiv = hi[0], idv = id[0], szv = sz[0], bov = bo[0];
+      int kv = kk[0], gv = gg[0];
 #pragma unroll
-      for (int q = NS - 1; q >= 0; --q)
-        if (bal[q]) first = q * 64 + __builtin_ctzll(bal[q]);
-      // commit the unchanged run [i, first)
+      for (int q = 1; q < NS; ++q)
+        if (qs == q) { rv = r[q]; lov = lo[q]; hiv = hi[q]; idv = id[q]; szv = sz[q]; bov = bo[q]; kv = kk[q]; gv = gg[q]; }
+      double bn;
+      int ks;
+      if (HS) {
+        bn = rv * idv + szv;
+        ks = 1;
+      } else {
+        const double tt = rv * rv;
+        const int fast = __builtin_amdgcn_readlane((int)(tt >= lov && tt <= hiv), l);
+        if (fast) {
+          ks = kv;
+          bn = kv == 0 ? 0.0 : (kv == FALLTHROUGH ? bov : rv * idv + szv);
+        } else {
+          const double ri = readlane_f64(rv, l);  // uniform inputs -> uniform result
+          const double boi = readlane_f64(bov, l);
+          ks = chain_slow(d, ri, xq[first], grp[first], pu[first], pz[first], sc.sigmaE, &bn, boi);
+          ++nslow;
+        }
+      }
+      const double delta = readlane_f64(bn - bov, l);
+      const int ksu = __builtin_amdgcn_readlane(ks, l);
+      const int gf = __builtin_amdgcn_readlane(gv, l);
+      const double *grow = Gl + gf * B;
 #pragma unroll
       for (int q = 0; q < NS; ++q) {
         const int pos = q * 64 + lane;
-        if (pos >= i && pos < first) { ksel[pos] = kk[q]; bnw[pos] = kk[q] == 0 ? 0.0 : bo[q]; }
-      }
-      if (first >= bs) break;
-      const int qs = first >> 6, own = first & 63;  // wave-uniform
-      double rv = 0, lov = 0, hiv = -1, dnv = 1, szv = 0, bov = 0;
-      int kv = 0;
-#pragma unroll
-      for (int q = 0; q < NS; ++q)
-        if (q == qs) { rv = r[q]; lov = lo[q]; hiv = hi[q]; dnv = dn[q]; szv = sz[q]; bov = bo[q]; kv = kk[q]; }
-      int ksel_v;
-      double bnew;
-      if (HS) {
-        ksel_v = 1;
-        bnew = rv / dnv + szv;  // HorseshoeR.cpp:234
-      } else {
-        const double tt = rv * rv;
-        const int fast_own = __builtin_amdgcn_readlane((int)(tt >= lov && tt <= hiv), own);
-        if (fast_own) {
-          ksel_v = kv;
-        } else {
-          // slow path: exact re-evaluation with the corrected dot (every lane evaluates its own
-          // slot qs; the owner's result is broadcast)
-          const int pos = qs * 64 + lane;
-          const int pc = pos < bs ? pos : 0;
-          const int g = grp[pc];
-          const int m = mrk[pc];
-          const double p = uniform(d.seed, T_MARKER, (uint32_t)(d.col_offset + m), it, 0);
-          Decision dc = decide_bayesr(rv, xq[pc], sc.sigmaE, d.sigmaGG[g], d.pi + (int64_t)g * d.K,
-                                      d.cva + g, d.G, d.K, p, false);
-          ksel_v = dc.k;
-          dnv = dc.denom;
-          szv = sqrt(sc.sigmaE / dc.denom) * pp[pc];
-        }
-        bnew = ksel_v == 0 ? 0.0 : (ksel_v == FALLTHROUGH ? bov : rv / dnv + szv);  // :226-228
-      }
-      const int KS = __builtin_amdgcn_readlane(ksel_v, own);
-      const double BN = readlane_f64(bnew, own);
-      const double BO = readlane_f64(bov, own);
-      int gfv = 0;
-#pragma unroll
-      for (int q = 0; q < NS; ++q)
-        if (q == qs) gfv = gg[q];
-      const int GF = __builtin_amdgcn_readlane(gfv, own);
-      if (lane == own) { ksel[first] = KS; bnw[first] = BN; }
-      const double delta = BN - BO;
-      if (delta != 0.0) {
-        const double *grow = Gl + (int64_t)GF * B;
-#pragma unroll
-        for (int q = 0; q < NS; ++q) {
-          const int pos = q * 64 + lane;
-          if (pos > first && pos < bs) r[q] = r[q] - grow[gg[q]] * delta;
-        }
+        if (pos == first) { bf[q] = bn; kf[q] = ksu; }
+        if (pos > first && delta != 0.0) r[q] = r[q] - grow[gg[q]] * delta;
       }
       i = first + 1;
     }
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      const int pos = q * 64 + lane;
+      if (pos < bs) { ksel[pos] = kf[q]; bnw[pos] = bf[q]; }
+    }
+    if (lane == 0 && nslow) atomicAdd(&d.sc->n_slow, (unsigned long long)nslow);
   }
   __syncthreads();
   // 4) write back, compact the changed markers into the pending list (position order)
@@ -746,13 +821,16 @@ __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it) {
     d.pend_bn[idx] = bnw[t];
   }
   const int npend = misc[0] + misc[1] + misc[2] + misc[3];
-  const int npad = (npend + 7) & ~7;
+  const int npad = (npend + 31) & ~31;  // k_stream reads the list in batches of 32
   if (t >= npend && t < npad) {  // neutral padding: eps + x*0 - x*0 == eps exactly
     d.pend_idx[t] = 0;
     d.pend_bo[t] = 0.0;
     d.pend_bn[t] = 0.0;
   }
-  if (t == 0) d.sc->n_pend = npad;
+  if (t == 0) {
+    d.sc->n_pend = npad;
+    if (npend) atomicAdd(&d.sc->n_changed, (unsigned long long)npend);
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -971,7 +1049,10 @@ hipError_t launch_sweep_start(const Dev &d, uint32_t it, hipStream_t st) {
 }
 
 hipError_t launch_perm(const Dev &d, uint32_t it, int shard, bool identity, hipStream_t st) {
-  if (!identity) hipLaunchKernelGGL(k_perm_blockorder, dim3(1), dim3(64), 0, st, d, it, shard);
+  if (!identity) {
+    const size_t lds = d.nb <= PERM_LDS_MAX ? sizeof(int) * (size_t)d.nb : 0;
+    hipLaunchKernelGGL(k_perm_blockorder, dim3(1), dim3(256), lds, st, d, it, shard);
+  }
   hipLaunchKernelGGL(k_perm_within, dim3((unsigned)d.nb), dim3(64), 0, st, d, it, identity ? 1 : 0);
   return hipGetLastError();
 }
@@ -982,11 +1063,14 @@ hipError_t launch_fixed(const Dev &d, uint32_t it, bool perm_on_device, hipStrea
 }
 
 hipError_t launch_stream(const Dev &d, int s, hipStream_t st) {
-  hipLaunchKernelGGL(k_stream, dim3((unsigned)d.RG), dim3(256), 0, st, d, s);
+  if (d.B == 64)
+    hipLaunchKernelGGL(k_stream<64>, dim3((unsigned)d.RG), dim3(256), 0, st, d, s);
+  else
+    hipLaunchKernelGGL(k_stream<128>, dim3((unsigned)d.RG), dim3(256), 0, st, d, s);
   return hipGetLastError();
 }
 
-size_t solve_lds_bytes(int B) { return (size_t)B * B * 8 + (size_t)B * 9 * 8 + (size_t)B * 5 * 4 + 64; }
+size_t solve_lds_bytes(int B) { return (size_t)B * B * 8 + (size_t)B * 10 * 8 + (size_t)B * 5 * 4 + 64; }
 
 hipError_t launch_solve(const Dev &d, int s, uint32_t it, hipStream_t st) {
   const size_t lds = solve_lds_bytes(d.B);
@@ -1012,7 +1096,8 @@ hipError_t set_solve_lds_limit(int /*B*/) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
   }
-  return hipSuccess;
+  return hipFuncSetAttribute((const void *)k_perm_blockorder, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)(sizeof(int) * PERM_LDS_MAX));
 }
 
 hipError_t launch_markers(const Dev &d, int mode, uint32_t it, hipStream_t st) {

@@ -377,12 +377,12 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   Dev &d = s->d;
   d.N = N; d.ld = (N + 63) / 64 * 64; d.M = M; d.M_total = M_total; d.col_offset = col_offset;
   d.K = K; d.G = groups; d.F = (int)F; d.B = B; d.nb = s->nb; d.model = model;
-  // streaming geometry: ~2 workgroups per CU, one row per thread
+  // streaming geometry: ~2 workgroups per CU, 4 consecutive rows per lane (R multiple of 4)
   const int64_t target = 2LL * cus;
-  d.R = (int)std::min<int64_t>(256, std::max<int64_t>(1, (N + target - 1) / target));
+  d.R = (int)std::min<int64_t>(256, std::max<int64_t>(4, ((N + target - 1) / target + 3) / 4 * 4));
   d.RG = (int)((N + d.R - 1) / d.R);
   d.NG = (d.RG + STREAM_GROUP - 1) / STREAM_GROUP;
-  const int NGpad = (d.NG + 7) / 8 * 8;  // k_solve reads slab2 in unconditional batches of 8
+  const int NGpad = (d.NG + 31) / 32 * 32;  // k_solve reads slab2 in unconditional batches of 32
   d.MRG = (int)((M + 255) / 256);
   const int64_t RGrows = (N + 255) / 256;
   int rc = 0;
@@ -390,8 +390,8 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   rc |= s->alloc(const_cast<double **>(&d.Y), N);
   rc |= s->alloc(const_cast<double **>(&d.fixed), N * std::max<int64_t>(F, 1));
   rc |= s->alloc(const_cast<double **>(&d.cva), (int64_t)groups * std::max(K - 1, 1));
-  rc |= s->alloc(&d.eps, N);
-  rc |= s->alloc(&d.eps_start, N);
+  rc |= s->alloc(&d.eps, d.ld);  // padded to ld rows (zeros): k_stream loads 4 rows per lane
+  rc |= s->alloc(&d.eps_start, d.ld);
   rc |= s->alloc(&d.beta, M);
   rc |= s->alloc(&d.xsq, M);
   rc |= s->alloc(&d.lambda, M);
@@ -426,6 +426,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   // every buffer a kernel may read before writing is zeroed here (recycled device memory
   // holds the previous session's values): slab2 pad rows, member padding, pending list
   bool ok = hipMemsetAsync(d.cnt1, 0, sizeof(int) * d.NG, s->st) == hipSuccess &&
+            hipMemsetAsync(d.eps, 0, sizeof(double) * d.ld, s->st) == hipSuccess &&
             hipMemsetAsync(d.slab2, 0, sizeof(double) * NGpad * B, s->st) == hipSuccess &&
             hipMemsetAsync(d.member, 0, sizeof(int) * s->nb * B, s->st) == hipSuccess &&
             hipMemsetAsync(d.gidx, 0, sizeof(int) * s->nb * B, s->st) == hipSuccess &&
@@ -782,6 +783,8 @@ int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
     case BRR_C2: *out = sc.c2; return 0;
     case BRR_SIGMAG: return d2h(s, out, s->d.sigmaGG, 1);
     case BRR_SUMSQ_BETA: return d2h(s, out, s->d.stats, 1);
+    case 100: *out = (double)sc.n_slow; return 0;     // diagnostics (not in brr.h)
+    case 101: *out = (double)sc.n_changed; return 0;
     default: set_error("unknown scalar %d", which); return -1;
   }
 }

@@ -201,6 +201,9 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms = dt / args.steps * 1e3
+    diag = {"slow_steps_per_sweep": s.scalar(100) / (args.warmup + args.steps),
+            "changed_per_sweep": s.scalar(101) / (args.warmup + args.steps),
+            "nonzero_frac": 1.0 - float(s.vector(L.VCOUNT)[0]) / P if model != L.MODEL_HORSESHOE else 1.0}
     value = args.steps / dt  # whole-job sweeps/s (every rank holds a shard of the same sweep)
 
     # roofline of the dominant kernel (k_stream): HIP events around every streaming launch on
@@ -231,7 +234,7 @@ def main():
             "data": "synthetic (on-device Binomial(2,f) genotypes, standardised; f32 X, f64 arithmetic)",
             "config": {"workload": cfg["workload"], "N": N, "P": P, "K": K, "groups": G,
                        "block_size": Bsz, "order": "blocked", "parallelism": f"column-shard x{world}",
-                       "setup_s": round(t_setup, 2)},
+                       "setup_s": round(t_setup, 2), "diag": diag},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -217,6 +217,8 @@ struct orc {
   double mu, sigmaE, sigmaF, tau, eta, c2;
   int32_t it;
   glibc_rand grand;
+  double *stats;      /* [sum b^2, sum b^2/lambda, betaAcum[G], v[G*K]] used by the epilogue */
+  double *deps;       /* shard_only: this shard's eps - eps_start */
 };
 
 static double *dalloc(int64_t n) { return (double *)calloc((size_t)(n > 0 ? n : 1), sizeof(double)); }
@@ -233,6 +235,7 @@ orc *orc_create(const orc_config *cfg) {
   if (o->G < 1) o->G = 1;
   o->F = cfg->model == ORC_GROUPS ? cfg->F : 0;
   if (o->c.n_shards < 1) o->c.n_shards = 1;
+  if (o->c.shard_only >= o->c.n_shards) o->c.shard_only = -1;
   if (o->c.block_size < 1) o->c.block_size = 256;
   o->seed = (uint64_t)(int64_t)cfg->seed;
   o->eps = dalloc(o->N);
@@ -249,6 +252,8 @@ orc *orc_create(const orc_config *cfg) {
   o->v = dalloc((int64_t)o->G * o->K);
   o->betaAcum = dalloc(o->G);
   o->alpha = dalloc(o->F);
+  o->stats = dalloc(2 + o->G + (int64_t)o->G * o->K);
+  o->deps = dalloc(o->N);
   o->order = (int32_t *)malloc(sizeof(int32_t) * (size_t)o->P);
   o->forder = (int32_t *)malloc(sizeof(int32_t) * (size_t)(o->F > 0 ? o->F : 1));
   for (int64_t i = 0; i < o->P; ++i) o->order[i] = (int32_t)i;
@@ -262,6 +267,7 @@ void orc_destroy(orc *o) {
   free(o->eps); free(o->ytilde); free(o->eps_start); free(o->eps_acc); free(o->beta);
   free(o->comp); free(o->xsq); free(o->lambda); free(o->hsv); free(o->sigmaGG); free(o->pi);
   free(o->v); free(o->betaAcum); free(o->alpha); free(o->order); free(o->forder);
+  free(o->stats); free(o->deps);
   free(o);
 }
 
@@ -519,6 +525,7 @@ static void marker_pass(orc *o) {
   for (int s = 0; s < o->c.n_shards; ++s) {
     int64_t off;
     int64_t ps = shard_range(o, s, &off);
+    if (o->c.shard_only >= 0 && s != o->c.shard_only) { pos += ps; continue; }
     memcpy(o->eps, o->eps_start, sizeof(double) * (size_t)N);
     for (int64_t j = 0; j < ps; ++j) {
       int64_t m = o->order[pos + j];
@@ -527,13 +534,38 @@ static void marker_pass(orc *o) {
     for (int64_t i = 0; i < N; ++i) o->eps_acc[i] += o->eps[i] - o->eps_start[i];
     pos += ps;
   }
+  if (o->c.shard_only >= 0) {  /* the caller sums eps_acc over processes */
+    memcpy(o->deps, o->eps_acc, sizeof(double) * (size_t)N);
+    return;
+  }
   for (int64_t i = 0; i < N; ++i) o->eps[i] = o->eps_start[i] + o->eps_acc[i];
 }
 
+/* statistics the epilogue needs, over this process's markers (all markers unless shard_only) */
+static void compute_stats(orc *o) {
+  const int G = o->G, K = o->K;
+  double *st = o->stats;
+  memset(st, 0, sizeof(double) * (size_t)(2 + G + G * K));
+  /* per-shard partial sums added in shard order: what an all-reduce over the shards' local
+   * statistics computes (exact match for two shards); one shard = one sequential sum */
+  for (int sh = 0; sh < o->c.n_shards; ++sh) {
+    if (o->c.shard_only >= 0 && sh != o->c.shard_only) continue;
+    int64_t m0;
+    const int64_t m1 = shard_range(o, sh, &m0) + m0;
+    double b2 = 0.0, b2l = 0.0;
+    for (int64_t m = m0; m < m1; ++m) b2 += o->beta[m] * o->beta[m];
+    if (o->c.model == ORC_HORSESHOE)
+      for (int64_t m = m0; m < m1; ++m) b2l += pow(o->beta[m], 2) / o->lambda[m];
+    st[0] += b2;
+    st[1] += b2l;
+  }
+  for (int g = 0; g < G; ++g) st[2 + g] = o->betaAcum[g];
+  for (int q = 0; q < G * K; ++q) st[2 + G + q] = o->v[q];
+}
+static void bayesr_epilogue(orc *o);
+
 static void sweep_bayesr(orc *o) {
-  const int64_t N = o->N, P = o->P;
   const int K = o->K, G = o->G;
-  const uint32_t it = (uint32_t)o->it;
   const orc_config *c = &o->c;
   mu_update(o);
   make_orders(o);
@@ -541,10 +573,23 @@ static void sweep_bayesr(orc *o) {
   memset(o->v, 0, sizeof(double) * (size_t)(G * K));
   memset(o->betaAcum, 0, sizeof(double) * (size_t)G);
   marker_pass(o);
+  compute_stats(o);
+  if (c->model != ORC_HORSESHOE && o->c.shard_only >= 0) return; /* epilogue after exchange */
+  bayesr_epilogue(o);
+}
+
+static void bayesr_epilogue(orc *o) {
+  const int64_t N = o->N, P = o->P;
+  const int K = o->K, G = o->G;
+  const uint32_t it = (uint32_t)o->it;
+  const orc_config *c = &o->c;
+  (void)N;
+  const double *v = o->stats + 2 + G;
+  const double *bacc = o->stats + 2;
   if (c->model == ORC_V2) {
     /* BayesRv2.cpp:247-255 */
-    const int m0 = (int)(P - (int64_t)o->v[0]);
-    const double bsq = sqnorm(o->beta, P);
+    const int m0 = (int)(P - (int64_t)v[0]);
+    const double bsq = o->stats[0];
     o->sigmaGG[0] = inv_scaled_chisq_rng(o->seed, c->v0G + m0,
                                          (bsq * m0 + c->v0G * c->s02G) / (c->v0G + m0),
                                          ORC_T_SIGMAG, 0, it);
@@ -552,7 +597,7 @@ static void sweep_bayesr(orc *o) {
                                      (sqnorm(o->eps, N) + c->v0E * c->s02E) / (c->v0E + N),
                                      ORC_T_SIGMAE, 0, it);
     double a[ORC_MAXK];
-    for (int k = 0; k < K; ++k) a[k] = o->v[k] + 1.0;
+    for (int k = 0; k < K; ++k) a[k] = v[k] + 1.0;
     dirichlet_rng(o->seed, a, K, o->pi, ORC_T_PI, 0, it);
   } else {
     if (c->model == ORC_GROUPS) {
@@ -567,21 +612,23 @@ static void sweep_bayesr(orc *o) {
                                      ORC_T_SIGMAE, 0, it);
     for (int g = 0; g < G; ++g) { /* Groups :307-312 / restart :257-262 */
       double rs = 0.0;
-      for (int k = 0; k < K; ++k) rs += o->v[g * K + k];
-      const int m0 = (int)(rs - o->v[g * K + 0]);
+      for (int k = 0; k < K; ++k) rs += v[g * K + k];
+      const int m0 = (int)(rs - v[g * K + 0]);
       o->sigmaGG[g] = inv_scaled_chisq_rng(
-          o->seed, c->v0G + m0, (o->betaAcum[g] * m0 + c->v0G * c->s02G) / (c->v0G + m0),
+          o->seed, c->v0G + m0, (bacc[g] * m0 + c->v0G * c->s02G) / (c->v0G + m0),
           ORC_T_SIGMAG, (uint32_t)g, it);
       double a[ORC_MAXK];
-      for (int k = 0; k < K; ++k) a[k] = o->v[g * K + k] + 1.0;
+      for (int k = 0; k < K; ++k) a[k] = v[g * K + k] + 1.0;
       dirichlet_rng(o->seed, a, K, o->pi + g * K, ORC_T_PI, (uint32_t)(g * K), it);
     }
   }
 }
 
+static void hs_epilogue(orc *o);
+
 static void sweep_horseshoe(orc *o) {
   /* HorseshoeR.cpp:210-253 */
-  const int64_t N = o->N, P = o->P;
+  const int64_t P = o->P;
   const uint32_t it = (uint32_t)o->it;
   const orc_config *c = &o->c;
   mu_update(o);
@@ -593,21 +640,57 @@ static void sweep_horseshoe(orc *o) {
     o->hsv[j] = inv_gamma_rate_rng(o->seed, 0.5 + 0.5 * c->vL, c->vL / o->lambda[j] + 1.0,
                                    ORC_T_HS_V, (uint32_t)j, it);
   marker_pass(o);                                                                   /* :219-240 */
-  for (int64_t j = 0; j < P; ++j)                                                   /* :242 */
+  int64_t j0 = 0, j1 = P;
+  if (o->c.shard_only >= 0) j1 = j0 + shard_range(o, o->c.shard_only, &j0);
+  for (int64_t j = j0; j < j1; ++j)                                                 /* :242 */
     o->lambda[j] = inv_gamma_rate_rng(
         o->seed, 0.5 + 0.5 * c->vL,
         c->vL * (1.0 / o->hsv[j]) + (0.5 * (o->beta[j] * o->beta[j])) * (1.0 / o->tau),
         ORC_T_HS_LAMBDA, (uint32_t)j, it);
-  double sb = 0.0;
-  for (int64_t j = 0; j < P; ++j) sb += pow(o->beta[j], 2) / o->lambda[j];
+  compute_stats(o);
+  if (o->c.shard_only >= 0) return; /* epilogue after exchange */
+  hs_epilogue(o);
+}
+
+static void hs_epilogue(orc *o) {
+  const int64_t N = o->N, P = o->P;
+  const uint32_t it = (uint32_t)o->it;
+  const orc_config *c = &o->c;
+  const double sb = o->stats[1];
   o->tau = inv_gamma_rate_rng(o->seed, 0.5 * (P + c->vT), c->vT / o->eta + (0.5) * sb,
                               ORC_T_HS_TAU, 0, it);                                 /* :245 */
   o->c2 = inv_gamma_rate_rng(o->seed, 0.5 * c->vC + 0.5 * P,
-                             c->vC * c->sC * 0.5 + 0.5 * sqnorm(o->beta, P), ORC_T_HS_C2, 0,
+                             c->vC * c->sC * 0.5 + 0.5 * o->stats[0], ORC_T_HS_C2, 0,
                              it);                                                   /* :248 */
   o->sigmaE = inv_scaled_chisq_rng(o->seed, c->v0E + N,
                                    (sqnorm(o->eps, N) + c->v0E * c->s02E) / (c->v0E + N),
                                    ORC_T_SIGMAE, 0, it);                            /* :253 */
+}
+
+int orc_sweep_local(orc *o) {
+  if (o->c.shard_only < 0) return -1;
+  if (o->c.model == ORC_HORSESHOE) sweep_horseshoe(o); else sweep_bayesr(o);
+  return 0;
+}
+
+int64_t orc_stats_size(const orc *o) { return 2 + o->G + (int64_t)o->G * o->K; }
+
+int orc_exchange_get(const orc *o, double *deps, double *stats) {
+  if (deps) memcpy(deps, o->deps, sizeof(double) * (size_t)o->N);
+  if (stats) memcpy(stats, o->stats, sizeof(double) * (size_t)orc_stats_size(o));
+  return 0;
+}
+
+int orc_exchange_set(orc *o, const double *deps_sum, const double *stats_sum) {
+  for (int64_t i = 0; i < o->N; ++i) o->eps[i] = o->eps_start[i] + deps_sum[i];
+  memcpy(o->stats, stats_sum, sizeof(double) * (size_t)orc_stats_size(o));
+  return 0;
+}
+
+int orc_sweep_finish(orc *o) {
+  if (o->c.model == ORC_HORSESHOE) hs_epilogue(o); else bayesr_epilogue(o);
+  o->it++;
+  return 0;
 }
 
 int orc_sweep(orc *o, int n) {

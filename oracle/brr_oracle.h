@@ -73,6 +73,8 @@ typedef struct orc_config {
   int32_t block_size;         /* B for ORC_ORDER_BLOCKED */
   int32_t n_shards;           /* column shards emulated (1 = single device) */
   const double *pi0;          /* optional G x K (row-major per group) initial pi override */
+  int32_t shard_only;         /* -1: emulate all n_shards in-process; s >= 0: this process
+                                 sweeps shard s only and exchanges through orc_exchange_* */
 } orc_config;
 
 typedef struct orc orc;
@@ -84,6 +86,14 @@ int orc_init(orc *o);
 /* n full sweeps (one iteration of the reference's `for(iteration...)` loop each) */
 int orc_sweep(orc *o, int n);
 int32_t orc_iteration(const orc *o);
+/* per-shard protocol (shard_only >= 0), the CPU restatement of brr_session_sweep_local /
+ * all-reduce / brr_session_sweep_finish: stats layout = [sum beta^2 (own markers),
+ * sum beta^2/lambda, betaAcum[G], v[G*K]] */
+int orc_sweep_local(orc *o);
+int64_t orc_stats_size(const orc *o);
+int orc_exchange_get(const orc *o, double *deps /* N */, double *stats);
+int orc_exchange_set(orc *o, const double *deps_sum, const double *stats_sum);
+int orc_sweep_finish(orc *o);
 
 /* state access. names: see orc_get_* in brr_oracle.c */
 enum {

@@ -44,6 +44,7 @@ class OrcConfig(C.Structure):
         ("eps0", C.POINTER(C.c_double)), ("comp0", C.POINTER(C.c_double)),
         ("seed", C.c_int32), ("order_mode", C.c_int32), ("block_size", C.c_int32),
         ("n_shards", C.c_int32), ("pi0", C.POINTER(C.c_double)),
+        ("shard_only", C.c_int32),
     ]
 
 
@@ -91,6 +92,12 @@ def lib():
                                   C.POINTER(C.c_double)]
         L.orc_synth_beta.argtypes = [C.c_uint64, C.c_int64, C.c_int64, C.c_int64, C.c_int64,
                                      C.POINTER(C.c_double)]
+        L.orc_sweep_local.argtypes = [C.c_void_p]
+        L.orc_sweep_finish.argtypes = [C.c_void_p]
+        L.orc_stats_size.restype = C.c_int64
+        L.orc_stats_size.argtypes = [C.c_void_p]
+        L.orc_exchange_get.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.orc_exchange_set.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.orc_run_csv.argtypes = [C.POINTER(OrcConfig), C.c_char_p, C.c_int, C.c_int, C.c_int]
         _lib = L
     return _lib
@@ -156,11 +163,11 @@ class Oracle:
     """One oracle chain. Arrays are kept alive on the instance (C holds raw pointers)."""
 
     def __init__(self, model, X=None, Y=None, *, cva=None, gAssign=None, fixed=None, G=1,
-                 seed=1, order_mode=ORDER_BLOCKED, block_size=256, n_shards=1,
+                 seed=1, order_mode=ORDER_BLOCKED, block_size=128, n_shards=1,
                  sigma0=0.01, v0E=1e-4, s02E=1e-3, v0G=1e-4, s02G=1e-3,
                  A=1.0, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0,
                  mu0=0.0, sigmaE0=1.0, beta0=None, sigmaGG0=None, eps0=None, comp0=None,
-                 pi0=None, N=None):
+                 pi0=None, N=None, shard_only=-1):
         self._keep = []
         X = np.asfortranarray(np.asarray(X, dtype=np.float64))
         if N is None:
@@ -199,6 +206,7 @@ class Oracle:
         cfg.order_mode = order_mode
         cfg.block_size = block_size
         cfg.n_shards = n_shards
+        cfg.shard_only = shard_only
         self.cfg = cfg
         self.N, self.P, self.K, self.G = N, P, cfg.K, G
         self.h = lib().orc_create(C.byref(cfg))
@@ -209,6 +217,24 @@ class Oracle:
     def sweep(self, n=1):
         lib().orc_sweep(self.h, n)
         return self
+
+    # per-shard protocol (shard_only >= 0): local sweep -> exchange -> finish
+    def sweep_local(self):
+        assert lib().orc_sweep_local(self.h) == 0
+
+    def exchange_get(self):
+        ns = lib().orc_stats_size(self.h)
+        e, s = np.zeros(self.N), np.zeros(ns)
+        lib().orc_exchange_get(self.h, _dptr(e), _dptr(s))
+        return e, s
+
+    def exchange_set(self, eps_sum, stats_sum):
+        e = np.ascontiguousarray(eps_sum, dtype=np.float64)
+        s = np.ascontiguousarray(stats_sum, dtype=np.float64)
+        lib().orc_exchange_set(self.h, _dptr(e), _dptr(s))
+
+    def sweep_finish(self):
+        lib().orc_sweep_finish(self.h)
 
     def scalar(self, which):
         return lib().orc_get_scalar(self.h, which)
