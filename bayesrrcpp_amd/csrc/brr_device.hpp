@@ -3,11 +3,18 @@
 // HBM layout (one session = one GPU = one column shard):
 //   X        f32, column-major, ld = roundup(N, 64) rows (256-B aligned columns); the only
 //            large array: streamed once per sweep by k_stream.
-//   eps      f64 [N] residual (Y - mu - X beta), owned row-wise by k_stream workgroups.
+//   eps,eps2 f64 [ld] residual (Y - mu - X beta), double-buffered across k_stream launches.
 //   beta,xsq f64 [M]; comp int32 [M]; sel uint8 [M] (marker selected a component this sweep)
 //   gram     f64 [nb][B][B] block Gram matrices X_b^T X_b of the fixed column blocks.
+//   xgram    f64 [nb][B][B] cross-Gram X_b^T X_{b+1 mod nb} of cycle neighbours; xgramT its
+//            transposes (rows indexed by block b+1).  Consecutive blocks of a sweep are cycle
+//            neighbours (visit order = rotation of the block cycle, either direction).
 //   member   int32 [nb*B] marker at (block position s, slot i); gidx = its row in the Gram.
-//   slab1/2  f64 partial dot products (2-level deterministic reduction, see k_stream).
+//   mc       f64 [fields][nb*B] per-marker constants of the sweep in visit order (k_prep).
+//   slab1/2  f64 partial dot products (2-level deterministic reduction, see k_stream), two
+//            copies (block parity): k_stream(s+1) runs while k_solve(s) reads copy s & 1.
+//   pend_*   changed markers of a block (three slots, block mod 3): written by k_solve(s),
+//            read by k_solve(s+1) (cross-Gram correction) and k_stream(s+2) (residual update).
 #pragma once
 #include <stdint.h>
 
@@ -15,7 +22,8 @@ namespace brr {
 
 constexpr int MAXK = 8;         // mixture components incl. zero
 constexpr int MAXG = 64;        // groups
-constexpr int BMAX = 128;       // marker block (f64 Gram block must fit LDS: 128 KiB)
+constexpr int BMAX = 512;       // marker block (Gram rows are staged in LDS on demand)
+constexpr int SROWS = 256;      // k_stream rows per workgroup (64 lanes x 4 rows: 1 KiB per column)
 constexpr int STREAM_GROUP = 16;  // k_stream workgroups per first-level reduction group
 constexpr int FALLTHROUGH = 255;  // no component selected (700-guard, BayesRv2.cpp:216-242)
 
@@ -26,10 +34,13 @@ struct Scal {
   double mu, mu_prev, sigmaE, sigmaF, tau, eta, c2;
   double S1;   // sum(eps + mu)   (BayesRv2.cpp:177-178 operand), from the latest row pass
   double S2;   // ||eps||^2        (BayesRv2.cpp:251 operand)
-  int n_pend;  // pending residual updates (previous block's changed markers)
-  int pad;
+  int pend_seq;  // blocks of the current sweep whose k_solve has published its changes
+  int err;       // device-side protocol error (a bounded wait timed out)
   unsigned long long n_slow;     // diagnostics: serial steps that needed the exact re-evaluation
   unsigned long long n_changed;  // diagnostics: markers whose beta changed
+  int prof_on;                   // diagnostics: k_solve phase timers on
+  int pad2;
+  unsigned long long prof[12];   // k_solve phase totals (wall_clock64 ticks, 100 MHz), counters
 };
 
 struct Hyper {
@@ -50,15 +61,20 @@ struct Dev {
   const float *X;
   const double *Y, *fixed, *cva;
   const int *gAssign;
-  double *eps, *eps_start, *deps, *beta, *xsq, *lambda, *hsv, *sigmaGG, *pi, *alpha;
+  double *eps, *eps2, *eps_start, *deps, *beta, *xsq, *lambda, *hsv, *sigmaGG, *pi, *alpha;
+  double *mc;       // per-position constants, field f at mc + f * nbB (see MC_* in brr_kernels.hip)
+  int64_t nbB;      // nb * B
   int *comp, *forder;
   uint8_t *sel;
-  double *gram;
+  double *gram, *xgram, *xgramT;
   int *member, *gidx, *bsz, *gblk, *blkorder;
-  double *slab1, *slab2;
-  int *cnt1;
-  int *pend_idx;
+  double *slab1, *slab2;   // [2][RG*B], [2][NGpad*B]
+  int *cnt1;                // [2][NG*NC] level-2 arrival counters (k_stream)
+  int *gdone;               // [2] level-2 groups completed (k_stream -> k_solve)
+  int64_t slab1_stride, slab2_stride, pend_stride;
+  int *pend_idx, *pend_gi;  // [3][B+16]
   double *pend_bo, *pend_bn;
+  int *pend_n;              // [3] padded counts (multiple of 16)
   double *rslab;
   int *rcnt;
   double *mslab;

@@ -89,6 +89,33 @@ __device__ __forceinline__ double ld_sc1(const double *p) {
   return __longlong_as_double(__hip_atomic_load(reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT));
 }
+__device__ __forceinline__ void st_sc1_int(int *p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_sc1_int(const int *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Bounded wait (one lane) for a device counter published by a kernel running concurrently on
+// the other queue.  Never spins forever: after ~0.5 s the protocol error flag is raised and the
+// caller proceeds (the host reports the error after the sweep).
+constexpr uint32_t SPIN_MAX = 1u << 22;
+__device__ __forceinline__ void wait_geq(const int *cnt, int target, int *err) {
+  for (uint32_t n = 0; ld_sc1_int(cnt) < target; ++n) {
+    if (n > SPIN_MAX) { atomicOr(err, 1); return; }
+    if ((n & 255) == 255 && ld_sc1_int(err)) return;  // an earlier wait already failed
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+// Publish a count after this workgroup's sc1 payload stores: every storing wave drains, then
+// one relaxed agent-scope add (MI355X_MICROARCH.md "Valid forms", row 1).
+__device__ __forceinline__ void publish_add(int *cnt, int v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ bool last_arriver_wt(int *cnt, int total, int *lds_flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
   __syncthreads();
@@ -178,17 +205,20 @@ __global__ void k_copy_f32(const float *src, int64_t lds, float *dst, int64_t ld
 }
 
 // ------------------------------------------------------------------------------------
-// Block Gram matrices: G[gb][i][j] = sum_r x(col(gb,i))[r] * x(col(gb,j))[r] in f64.
-// 64x64 output tile per workgroup, 4x4 per thread, 64-row chunks staged in LDS.
-// Element (i,j) and (j,i) accumulate identical products in identical order -> symmetric.
+// Block Gram matrices: G[b][i][j] = sum_r x(col(b,i))[r] * x(col(b2,j))[r] in f64 with
+// b2 = (b + shift) mod nb: shift 0 gives the diagonal blocks X_b^T X_b, shift 1 the cross-Gram
+// of cycle neighbours (also stored transposed in GT when GT != nullptr).  64x64 output tile per
+// workgroup, 4x4 per thread, 64-row chunks staged in LDS.  Element (i,j) and (j,i) of a
+// diagonal block accumulate identical products in identical order -> exactly symmetric.
 __global__ __launch_bounds__(256) void k_gram(const float *X, int64_t ld, const int *member,
-                                              const int *bsz, int B, double *G) {
+                                              const int *bsz, int B, int nb, int shift, double *G, double *GT) {
   __shared__ float As[64][65];
   __shared__ float Bs[64][65];
   const int gb = blockIdx.x;
+  const int gb2 = (gb + shift) % nb;
   const int ntile = (B + 63) / 64;
   const int ti = blockIdx.y / ntile, tj = blockIdx.y % ntile;
-  const int bs = bsz[gb];
+  const int bs = bsz[gb], bs2 = bsz[gb2];
   const int t = threadIdx.x;
   const int ty = t >> 4, tx = t & 15;
   double acc[4][4];
@@ -200,7 +230,7 @@ __global__ __launch_bounds__(256) void k_gram(const float *X, int64_t ld, const 
   const int lc = t >> 2, lr = (t & 3) * 16;
   const int ci = ti * 64 + lc, cj = tj * 64 + lc;
   const float *pa = (ci < bs) ? X + (int64_t)member[(int64_t)gb * B + ci] * ld : nullptr;
-  const float *pb = (cj < bs) ? X + (int64_t)member[(int64_t)gb * B + cj] * ld : nullptr;
+  const float *pb = (cj < bs2) ? X + (int64_t)member[(int64_t)gb2 * B + cj] * ld : nullptr;
   for (int64_t r0 = 0; r0 < ld; r0 += 64) {
 #pragma unroll
     for (int q = 0; q < 16; q += 4) {
@@ -223,12 +253,17 @@ __global__ __launch_bounds__(256) void k_gram(const float *X, int64_t ld, const 
     __syncthreads();
   }
   double *g = G + (int64_t)gb * B * B;
+  double *gt = GT ? GT + (int64_t)gb * B * B : nullptr;
 #pragma unroll
   for (int p = 0; p < 4; ++p)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int i = ti * 64 + ty * 4 + p, jj = tj * 64 + tx * 4 + q;
-      if (i < B && jj < B) g[(int64_t)i * B + jj] = (i < bs && jj < bs) ? acc[p][q] : 0.0;
+      if (i < B && jj < B) {
+        const double v = (i < bs && jj < bs2) ? acc[p][q] : 0.0;
+        g[(int64_t)i * B + jj] = v;
+        if (gt) gt[(int64_t)jj * B + i] = v;
+      }
     }
 }
 
@@ -248,7 +283,8 @@ enum RowFlags : int {
   ROW_EXCHANGE = 32, ROW_REDUCE = 64, ROW_INIT_Y = 128
 };
 
-__global__ __launch_bounds__(256) void k_rows(Dev d, int flags, const double *deps_in) {
+__global__ __launch_bounds__(256) void k_rows(Dev d, int flags, const double *deps_in, const double *eps_in,
+                                              int slot_a, int slot_b) {
 #pragma clang fp contract(off)
   __shared__ double red[8];
   __shared__ int s_last;
@@ -258,18 +294,26 @@ __global__ __launch_bounds__(256) void k_rows(Dev d, int flags, const double *de
   if (valid) {
     if (flags & ROW_INIT_Y) e = d.Y[row] - d.sc->mu - 0.0;  // eps = Y - mu - X*beta, beta=0
     else if (flags & ROW_EXCHANGE) e = d.eps_start[row] + deps_in[row];
-    else e = d.eps[row];
+    else e = (eps_in ? eps_in : d.eps)[row];
   }
   if (flags & ROW_SHIFT) e = (e + d.sc->mu_prev) - d.sc->mu;
   if (flags & ROW_PENDING) {
-    const int np = d.sc->n_pend;  // multiple of 8, neutral padding
+    // the last one or two blocks' changes (slots slot_a then slot_b; -1 = none), lists padded
+    // to a multiple of 16 with neutral entries
     const float *Xr = d.X + (valid ? row : 0);
-    for (int p0 = 0; p0 < np; p0 += 8) {
-      double x[8];
+    for (int k = 0; k < 2; ++k) {
+      const int slot = k == 0 ? slot_a : slot_b;
+      if (slot < 0) continue;
+      const int np = d.pend_n[slot];
+      const int *pidx = d.pend_idx + slot * d.pend_stride;
+      const double *pbo = d.pend_bo + slot * d.pend_stride, *pbn = d.pend_bn + slot * d.pend_stride;
+      for (int p0 = 0; p0 < np; p0 += 8) {
+        double x[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) x[q] = (double)Xr[(int64_t)d.pend_idx[p0 + q] * d.ld];
+        for (int q = 0; q < 8; ++q) x[q] = (double)Xr[(int64_t)pidx[p0 + q] * d.ld];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) e = (e + x[q] * d.pend_bo[p0 + q]) - x[q] * d.pend_bn[p0 + q];
+        for (int q = 0; q < 8; ++q) e = (e + x[q] * pbo[p0 + q]) - x[q] * pbn[p0 + q];
+      }
     }
   }
   if (valid) {
@@ -302,7 +346,9 @@ __global__ void k_sweep_start(Dev d, uint32_t it) {
   sc->mu_prev = sc->mu;
   const double z = normal(d.seed, T_MU, 0, it, 0);
   sc->mu = sc->S1 / (double)d.N + sqrt(sc->sigmaE / (double)d.N) * z;
-  sc->n_pend = 0;
+  sc->pend_seq = 0;
+  d.gdone[0] = 0;
+  d.gdone[1] = 0;
   if (d.model == MODEL_HORSESHOE) {
     const Hyper &h = d.hyp;
     sc->eta = inv_gamma_rate_rng(d.seed, 0.5 + 0.5 * h.vT,
@@ -324,27 +370,20 @@ __device__ void fisher_yates_dev(uint64_t seed, int *a, int n, uint32_t tag, uin
   }
 }
 
-// Block order: Fisher-Yates in LDS (serial by definition), then one coalesced write.
-constexpr int PERM_LDS_MAX = 32768;  // blocks per shard handled in LDS (128 KiB)
-__global__ __launch_bounds__(256) void k_perm_blockorder(Dev d, uint32_t it, int shard) {
-  extern __shared__ __attribute__((aligned(16))) int ord[];
-  const int nb = d.nb;
-  if (nb <= PERM_LDS_MAX) {
-    for (int b = threadIdx.x; b < nb; b += blockDim.x) ord[b] = b;
-    __syncthreads();
-    if (threadIdx.x == 0) fisher_yates_dev(d.seed, ord, nb, T_PERM_BLOCK, (uint32_t)shard, it);
-    __syncthreads();
-    for (int b = threadIdx.x; b < nb; b += blockDim.x) d.blkorder[b] = ord[b];
-  } else if (threadIdx.x == 0) {
-    for (int b = 0; b < nb; ++b) d.blkorder[b] = b;
-    fisher_yates_dev(d.seed, d.blkorder, nb, T_PERM_BLOCK, (uint32_t)shard, it);
-  }
+// Block order: a rotation of the block cycle, forwards or backwards (Philox draw, entity =
+// shard), so consecutive blocks of a sweep are cycle neighbours (cross-Gram precomputed).
+__global__ __launch_bounds__(256) void k_perm_blockorder(Dev d, uint32_t it, int shard, int identity) {
+  const int64_t nb = d.nb;
+  const uint4 w = philox(d.seed, 0, T_PERM_BLOCK, (uint32_t)shard, it);
+  const int64_t rot = identity ? 0 : (int64_t)(((uint64_t)w.x * (uint64_t)nb) >> 32);
+  const int64_t dir = identity ? 1 : ((w.y & 1u) ? 1 : -1);
+  for (int64_t s = threadIdx.x; s < nb; s += blockDim.x) d.blkorder[s] = (int)(((rot + dir * s) % nb + nb) % nb);
 }
 
 __global__ void k_perm_within(Dev d, uint32_t it, int identity) {
   __shared__ int w[BMAX];
   const int s = blockIdx.x;
-  const int b = identity ? s : d.blkorder[s];
+  const int b = d.blkorder[s];
   const int size = (int)min((int64_t)d.B, d.M - (int64_t)b * d.B);
   for (int i = threadIdx.x; i < size; i += blockDim.x) w[i] = i;
   __syncthreads();
@@ -397,135 +436,6 @@ __global__ __launch_bounds__(1024) void k_fixed(Dev d, uint32_t it, int perm_on_
 }
 
 // ------------------------------------------------------------------------------------
-// k_stream: residual update for the previous block + partial dots for block position s.
-// grid = RG workgroups, each owns rows [rg*R, rg*R + R) (R <= 256, one row per thread).
-// Partial dots: 32 columns at a time, wave transpose-reduction (32 shuffles / 32 columns),
-// cross-wave via LDS -> slab1[rg][c]; the last of each group of STREAM_GROUP workgroups
-// sums its group's rows -> slab2[group][c] (read by k_solve).
-__device__ __forceinline__ double wave_reduce32(double (&v)[32], int lane) {
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const bool hi = lane & 32;
-    const double send = hi ? v[j] : v[j + 16];
-    const double keep = hi ? v[j + 16] : v[j];
-    v[j] = keep + __shfl_xor(send, 32);
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const bool hi = lane & 16;
-    const double send = hi ? v[j] : v[j + 8];
-    const double keep = hi ? v[j + 8] : v[j];
-    v[j] = keep + __shfl_xor(send, 16);
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const bool hi = lane & 8;
-    const double send = hi ? v[j] : v[j + 4];
-    const double keep = hi ? v[j + 4] : v[j];
-    v[j] = keep + __shfl_xor(send, 8);
-  }
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const bool hi = lane & 4;
-    const double send = hi ? v[j] : v[j + 2];
-    const double keep = hi ? v[j + 2] : v[j];
-    v[j] = keep + __shfl_xor(send, 4);
-  }
-  {
-    const bool hi = lane & 2;
-    const double send = hi ? v[0] : v[1];
-    const double keep = hi ? v[1] : v[0];
-    v[0] = keep + __shfl_xor(send, 2);
-  }
-  return v[0] + __shfl_xor(v[0], 1);
-}
-
-__device__ __forceinline__ int reduce32_col(int lane) {
-  return ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 +
-         ((lane >> 2) & 1) * 2 + ((lane >> 1) & 1);
-}
-
-// Geometry: workgroup rg owns rows [rg*R, rg*R + R), R <= 256 a multiple of 4; lane l owns the
-// 4 consecutive rows rg*R + 4l .. +3 (one 16-B load per column), wave w owns the B/4 columns
-// [w B/4, (w+1) B/4) of the block.  X and eps are padded to ld rows (zeros), so every load is
-// unconditional.  The residual update is applied redundantly by the 4 waves (the re-read
-// columns hit the CU's L1/L2) and written back by wave 0: no barrier in the streaming part.
-template <int B>
-__global__ __launch_bounds__(256, 2) void k_stream(Dev d, int s) {
-#pragma clang fp contract(off)
-  constexpr int CW = B / 4;  // columns per wave (<= 32)
-  __shared__ int s_last;
-  const int t = threadIdx.x;
-  const int lane = t & 63, w = t >> 6;
-  const int rg = blockIdx.x;
-  const int64_t row0 = (int64_t)rg * d.R + 4 * lane;
-  const bool valid = 4 * lane < d.R && row0 < d.N;
-  const int64_t rowc = valid ? row0 : 0;
-  const float *Xr = d.X + rowc;
-  const int64_t ld = d.ld;
-  // block columns first: their loads do not depend on the residual update
-  const int *mem = d.member + (int64_t)s * B + w * CW;
-  float4 x[CW];
-#pragma unroll
-  for (int j = 0; j < CW; ++j) x[j] = *reinterpret_cast<const float4 *>(Xr + (int64_t)mem[j] * ld);
-  const double2 ea = *reinterpret_cast<const double2 *>(d.eps + rowc);
-  const double2 eb = *reinterpret_cast<const double2 *>(d.eps + rowc + 2);
-  double e0 = ea.x, e1 = ea.y, e2 = eb.x, e3 = eb.y;
-  // residual update for the previous block's changed markers, eps = (eps + x b_old) - x b_new
-  // (BayesRv2.cpp:191,243); list padded to a multiple of 32 with neutral b_old = b_new = 0
-  const int np = d.sc->n_pend;
-  for (int p0 = 0; p0 < np; p0 += 16) {
-    float4 xp[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) xp[q] = *reinterpret_cast<const float4 *>(Xr + (int64_t)d.pend_idx[p0 + q] * ld);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const double bo = d.pend_bo[p0 + q], bn = d.pend_bn[p0 + q];
-      const double a0 = xp[q].x, a1 = xp[q].y, a2 = xp[q].z, a3 = xp[q].w;
-      e0 = (e0 + a0 * bo) - a0 * bn;
-      e1 = (e1 + a1 * bo) - a1 * bn;
-      e2 = (e2 + a2 * bo) - a2 * bn;
-      e3 = (e3 + a3 * bo) - a3 * bn;
-    }
-  }
-  if (np > 0 && w == 0 && valid) {
-    *reinterpret_cast<double2 *>(d.eps + row0) = make_double2(e0, e1);
-    *reinterpret_cast<double2 *>(d.eps + row0 + 2) = make_double2(e2, e3);
-  }
-  if (!valid) e0 = e1 = e2 = e3 = 0.0;
-  // partial dots: 4 rows per lane, then the wave transpose-reduction over the 64 lanes
-  double v[32];
-#pragma unroll
-  for (int j = 0; j < 32; ++j) {
-    if (j < CW) {
-      v[j] = (((double)x[j].x * e0 + (double)x[j].y * e1) + (double)x[j].z * e2) + (double)x[j].w * e3;
-    } else {
-      v[j] = 0.0;
-    }
-  }
-  const double r = wave_reduce32(v, lane);
-  const int col = reduce32_col(lane);
-  if ((lane & 1) == 0 && col < CW) st_sc1(d.slab1 + (int64_t)rg * B + w * CW + col, r);
-  // level-2: last arriver of the group sums the group's partials in workgroup order
-  const int bs = d.bsz[s];
-  const int grp = rg / STREAM_GROUP;
-  const int g0 = grp * STREAM_GROUP;
-  const int gsz = min(STREAM_GROUP, d.RG - g0);
-  if (last_arriver_wt(d.cnt1 + grp, gsz, &s_last)) {
-    if (t < bs) {
-      double v16[STREAM_GROUP];
-#pragma unroll
-      for (int q = 0; q < STREAM_GROUP; ++q) v16[q] = q < gsz ? ld_sc1(d.slab1 + (int64_t)(g0 + q) * B + t) : 0.0;
-      double acc = 0.0;
-#pragma unroll
-      for (int q = 0; q < STREAM_GROUP; ++q) acc += v16[q];
-      d.slab2[(int64_t)grp * B + t] = acc;
-    }
-    if (t == 0) d.cnt1[grp] = 0;
-  }
-}
-
-// ------------------------------------------------------------------------------------
 // Per-marker mixture decision, restating BayesRv2.cpp:195-242 exactly (f64).
 // Returns the selected component (0..K-1) or FALLTHROUGH, and the quantities needed to
 // bound the t = num^2 interval in which the decision cannot change.
@@ -535,7 +445,7 @@ struct Decision {
   double margin;  // half-width in t = num^2 of a decision-invariant interval (0 = none)
 };
 
-__device__ Decision decide_bayesr(double num, double xsq, double sigmaE, double sigmaG,
+__device__ __forceinline__ Decision decide_bayesr(double num, double xsq, double sigmaE, double sigmaG,
                                   const double *pi_g, const double *cva_g /* stride Gs */,
                                   int Gs, int K, double p, bool want_margin) {
 #pragma clang fp contract(off)
@@ -623,213 +533,701 @@ __device__ Decision decide_bayesr(double num, double xsq, double sigmaE, double 
 }
 
 // ------------------------------------------------------------------------------------
-// k_solve: one workgroup.  Exact single-site updates of block position s in visit order.
-// Slow path of the serial chain: exact re-evaluation (reference formula) of position i with
-// its corrected dot product, when the corrected num^2 left the decision-invariant interval.
-__device__ __forceinline__ int chain_slow(const Dev &d, double num, double x2, int g,
-                                                    double p, double z, double sigmaE,
-                                                    double *bnew, double bold) {
-  Decision dc = decide_bayesr(num, x2, sigmaE, d.sigmaGG[g], d.pi + (int64_t)g * d.K, d.cva + g, d.G,
-                              d.K, p, false);
-  *bnew = dc.k == 0 ? 0.0 : (dc.k == FALLTHROUGH ? bold : num / dc.denom + sqrt(sigmaE / dc.denom) * z);
-  return dc.k;
+// Per-position constants of a sweep (k_prep), field-major mc[f * nbB + s * B + i] in visit
+// order.  BayesR: p (uniform), z (normal), beta_old, xsq, a_0..a_{K-1}, den_1..den_{K-1} with
+//   logL_k(t) = a_k + t / (2 den_k sigmaE),  t = num^2           (BayesRv2.cpp:200-209)
+//   a_0 = log pi_0,  a_k = log pi_k - 0.5 log((sigmaG/sigmaE) xsq cVa_k + 1),
+//   den_k = xsq + (sigmaE/sigmaG) / cVa_k                          (denom[k-1], :200)
+// Horseshoe: z, beta_old, xsq, D = xsq + sigmaE / (tau c2 lambda / (tau lambda + c2))
+// (HorseshoeR.cpp:226-234).  sigmaE, sigmaG, pi, tau, c2, lambda are constant during the
+// marker loop, and a marker's beta only changes at its own visit.
+enum McField : int { MC_P = 0, MC_Z = 1, MC_BO = 2, MC_XSQ = 3, MC_A = 4 };
+
+template <bool HS>
+__global__ __launch_bounds__(256) void k_prep(Dev d, uint32_t it) {
+#pragma clang fp contract(off)
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= d.nbB) return;
+  const int s = (int)(q / d.B), i = (int)(q % d.B);
+  if (i >= d.bsz[s]) return;
+  const int m = d.member[q];
+  const uint32_t gm = (uint32_t)(d.col_offset + m);
+  const int64_t S = d.nbB;
+  double *mc = d.mc;
+  const double bo = d.beta[m], x2 = d.xsq[m];
+  const double sigmaE = d.sc->sigmaE;
+  mc[MC_Z * S + q] = normal(d.seed, T_MARKER, gm, it, 1);
+  mc[MC_BO * S + q] = bo;
+  mc[MC_XSQ * S + q] = x2;
+  if (HS) {
+    const double lam = d.lambda[m], tau = d.sc->tau, c2 = d.sc->c2;
+    const double sv = tau * c2 * lam / (tau * lam + c2);
+    mc[MC_A * S + q] = x2 + (sigmaE / sv);
+  } else {
+    const int K = d.K, G = d.G;
+    const int g = d.gAssign ? d.gAssign[m] : 0;
+    const double sigmaG = d.sigmaGG[g];
+    const double *pi_g = d.pi + (int64_t)g * K;
+    mc[MC_P * S + q] = uniform(d.seed, T_MARKER, gm, it, 0);
+    mc[MC_A * S + q] = log(pi_g[0]);
+    for (int k = 1; k < K; ++k) {
+      const double cVa = d.cva[g + (int64_t)G * (k - 1)];
+      const double cVaI = 1.0 / cVa;
+      mc[(MC_A + K + k - 1) * S + q] = x2 + (sigmaE / sigmaG) * cVaI;
+      mc[(MC_A + k) * S + q] = log(pi_g[k]) - 0.5 * log(((sigmaG / sigmaE) * x2) * cVa + 1.0);
+    }
+  }
 }
 
-template <bool HS, int B>
-__global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it) {
+// Fast decision at num = r from the precomputed constants: P = softmax(logL(t)), A_k its
+// cumulative sums, selected k = first with p <= A_k.  Also returns a decision-invariant
+// window [lo, hi] in t (DESIGN.md "decision margins"): with logL_j = a_j + b_j t,
+//   dA_k/dt = A_k (1 - A_k)(bbar_{<=k} - bbar_{>k}),  |.| <= min(A_k, 1-A_k) b_max,
+// and over |t - t0| <= delta <= 1/b_max, A_k and 1-A_k grow by at most e^{b_max delta} <= e,
+// so A_k stays on its side of p while delta <= gap / (e b_max min(A_k, 1-A_k)); half of that
+// is used.  The reference's arithmetic differs from the softmax by a few ulps, so any gap
+// below 1e-12 -- and any spread of logL near the 700-guard (BayesRv2.cpp:212-240) -- is
+// handed to the exact evaluation (ex = true).
+struct FastDec {
+  int k;
+  double lo, hi;
+  bool ex;
+};
+
+__device__ __forceinline__ FastDec decide_fast(double r, const double *a, const double *den, int64_t stride, int K,
+                                               double sigmaE, double p) {
 #pragma clang fp contract(off)
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  double *Gl = reinterpret_cast<double *>(smem);  // B*B
-  double *r_ = Gl + (int64_t)B * B;                 // B each:
-  double *tlo = r_ + B, *thi = tlo + B, *ide = thi + B, *sdz = ide + B, *bold = sdz + B,
-         *bnw = bold + B, *pz = bnw + B, *xq = pz + B, *pu = xq + B;
-  int *k0 = reinterpret_cast<int *>(pu + B);
-  int *gi = k0 + B, *grp = gi + B, *ksel = grp + B, *mrk = ksel + B, *misc = mrk + B;
+  FastDec o;
+  o.ex = false;
+  const double t = r * r;
+  if (K == 1) { o.k = 0; o.lo = -1e308; o.hi = 1e308; return o; }
+  double L[MAXK], A[MAXK];
+  double mx = -1e308, mn = 1e308, smax = 0.0;
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) {
+    if (k < K) {
+      const double sl = k == 0 ? 0.0 : 0.5 / (den[(k - 1) * stride] * sigmaE);
+      L[k] = a[k * stride] + sl * t;
+      mx = fmax(mx, L[k]);
+      mn = fmin(mn, L[k]);
+      smax = fmax(smax, sl);
+    }
+  }
+  if (!(mx - mn < 690.0) || !(smax > 0.0)) { o.ex = true; o.k = 0; o.lo = 1.0; o.hi = -1.0; return o; }
+  double S = 0.0;
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) {
+    if (k < K) { A[k] = exp(L[k] - mx); S += A[k]; }
+  }
+  double acc = 0.0;
+  int sel = FALLTHROUGH;
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) {
+    if (k < K) {
+      acc += A[k];
+      A[k] = acc / S;
+      if (sel == FALLTHROUGH && p <= A[k]) sel = k;
+    }
+  }
+  const double E = 2.718281828459045;
+  auto side = [&](double gap, double Ak) -> double {
+    if (!(gap > 1e-12)) return 0.0;
+    const double m = fmin(Ak, 1.0 - Ak);
+    return m > 0.0 ? gap / (E * smax * m) : 1e300;
+  };
+  double w;
+  if (sel == FALLTHROUGH) {
+    w = 0.0;  // p above the last cumulative sum: only the exact formula decides
+  } else {
+    double Asel = A[0], Aprev = 0.0;
+#pragma unroll
+    for (int k = 1; k < MAXK; ++k)
+      if (k == sel) { Asel = A[k]; Aprev = A[k - 1]; }
+    w = side(Asel - p, Asel);
+    if (sel > 0) w = fmin(w, side(p - Aprev, Aprev));
+  }
+  w = fmin(w, 1.0 / smax);
+  const double mg = 0.5 * w;
+  o.k = sel;
+  if (!(mg > 0.0)) { o.ex = true; o.lo = 1.0; o.hi = -1.0; return o; }
+  o.lo = t - mg;
+  o.hi = t + mg;
+  return o;
+}
+
+// Decision with the window, exact fallback included (parallel phases: prep and refresh).
+__device__ __forceinline__ FastDec decide_pos(const Dev &d, double r, const double *a, const double *den, int64_t stride,
+                                              double sigmaE, double p, double x2, int m) {
+  FastDec o = decide_fast(r, a, den, stride, d.K, sigmaE, p);
+  if (o.ex) {
+    const int g = d.gAssign ? d.gAssign[m] : 0;
+    Decision dc = decide_bayesr(r, x2, sigmaE, d.sigmaGG[g], d.pi + (int64_t)g * d.K, d.cva + g, d.G, d.K, p, true);
+    if (dc.margin > 0.0) {
+      const double t = r * r;
+      o.k = dc.k;
+      o.lo = t - dc.margin;
+      o.hi = t + dc.margin;
+      o.ex = false;
+    }
+  }
+  return o;
+}
+
+// ------------------------------------------------------------------------------------
+// k_stream(s): residual update for block s-2 + partial dots of block s (lag-1 pipeline).
+// While k_solve(s-1) runs on the other queue, k_stream(s) forms d = X_s^T E_{s-1}, with E_t
+// the residual at the start of block t: it reads E_{s-2} (written by k_stream(s-1)), applies
+// block s-2's changes (published by k_solve(s-2)) and writes E_{s-1} to the other buffer.
+// k_solve(s) then subtracts the cross-Gram term X_s^T X_{s-1} delta_{s-1} exactly.
+// Tile = SROWS (256) rows x 4*CW columns; lane l owns the 4 consecutive rows 4l..4l+3 of the
+// tile (one 16-B load per column: 1 KiB = 8 whole 128-B lines per column and wave), wave w
+// owns CW columns.  Partial dots: wave transpose-reduction (32 shuffles / 32 columns) ->
+// slab1[rg][col]; the last of each group of STREAM_GROUP row tiles sums its group's rows ->
+// slab2[group][col] and counts the group in gdone (read by k_solve(s)).
+__device__ __forceinline__ double wave_reduce32(double (&v)[32], int lane) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const bool hi = lane & 32;
+    const double send = hi ? v[j] : v[j + 16];
+    const double keep = hi ? v[j + 16] : v[j];
+    v[j] = keep + __shfl_xor(send, 32);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bool hi = lane & 16;
+    const double send = hi ? v[j] : v[j + 8];
+    const double keep = hi ? v[j + 8] : v[j];
+    v[j] = keep + __shfl_xor(send, 16);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool hi = lane & 8;
+    const double send = hi ? v[j] : v[j + 4];
+    const double keep = hi ? v[j + 4] : v[j];
+    v[j] = keep + __shfl_xor(send, 8);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const bool hi = lane & 4;
+    const double send = hi ? v[j] : v[j + 2];
+    const double keep = hi ? v[j + 2] : v[j];
+    v[j] = keep + __shfl_xor(send, 4);
+  }
+  {
+    const bool hi = lane & 2;
+    const double send = hi ? v[0] : v[1];
+    const double keep = hi ? v[1] : v[0];
+    v[0] = keep + __shfl_xor(send, 2);
+  }
+  return v[0] + __shfl_xor(v[0], 1);
+}
+
+__device__ __forceinline__ int reduce32_col(int lane) {
+  return ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 +
+         ((lane >> 2) & 1) * 2 + ((lane >> 1) & 1);
+}
+
+// Grid: roundup(RG, 8) * NC workgroups, NC = B / (4 CW) column chunks.  Workgroup ids are
+// dispatched round-robin over the 8 XCDs; the mapping puts the NC chunks of one row tile on
+// the same XCD (bid % 8 == rg % 8), so the redundant residual update of the tile (each chunk
+// applies it to its own copy of the rows) re-reads the changed columns and eps from one L2.
+// Only chunk 0 writes eps_out, and no workgroup reads eps_out, so the update is race-free.
+// X and eps are padded to ld rows.
+template <int CW>
+__global__ __launch_bounds__(256, 2) void k_stream(Dev d, int s, const double *eps_in, double *eps_out) {
+#pragma clang fp contract(off)
+  constexpr int CB = 4 * CW;  // columns per workgroup
+  __shared__ int s_last, s_np;
+  __shared__ int s_pidx[BMAX + 16];
+  __shared__ double s_pbo[BMAX + 16], s_pbn[BMAX + 16];
+  const int t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6;
+  const int B = d.B;
+  const int NC = B / CB;
+  const int bid = blockIdx.x;
+  const int rest = bid >> 3;
+  const int cc = rest % NC;
+  const int rg = (rest / NC) * 8 + (bid & 7);
+  if (rg >= d.RG) return;
+  const int64_t row0 = (int64_t)rg * SROWS + 4 * lane;
+  const bool valid = row0 < d.N;
+  const int64_t rowc = valid ? row0 : 0;
+  const float *Xr = d.X + rowc;
+  const int64_t ld = d.ld;
+  const int par = s & 1;
+  // block columns first: their loads depend on nothing
+  const int *mem = d.member + (int64_t)s * B + cc * CB + w * CW;
+  float4 x[CW];
+#pragma unroll
+  for (int j = 0; j < CW; ++j) x[j] = *reinterpret_cast<const float4 *>(Xr + (int64_t)mem[j] * ld);
+  const double2 ea = *reinterpret_cast<const double2 *>(eps_in + rowc);
+  const double2 eb = *reinterpret_cast<const double2 *>(eps_in + rowc + 2);
+  double e0 = ea.x, e1 = ea.y, e2 = eb.x, e3 = eb.y;
+  // residual update for block s-2, eps = (eps + x b_old) - x b_new (BayesRv2.cpp:191,243): wait
+  // until k_solve(s-2) has published (normally long done), then read its list with sc1 loads;
+  // lists are padded to a multiple of 16 with neutral b_old = b_new = 0
+  if (s >= 2) {
+    // one wave stages the list in LDS (one sc1 request per line per workgroup, instead of one
+    // per wave and entry hammering the same few lines from every workgroup)
+    if (w == 0) {
+      if (lane == 0) wait_geq(&d.sc->pend_seq, s - 1, &d.sc->err);
+      const int slot = (s - 2) % 3;
+      const int np = ld_sc1_int(d.pend_n + slot);
+      const int *pidx = d.pend_idx + slot * d.pend_stride;
+      const double *pbo = d.pend_bo + slot * d.pend_stride, *pbn = d.pend_bn + slot * d.pend_stride;
+      for (int e = lane; e < np; e += 64) {
+        s_pidx[e] = ld_sc1_int(pidx + e);
+        s_pbo[e] = ld_sc1(pbo + e);
+        s_pbn[e] = ld_sc1(pbn + e);
+      }
+      if (lane == 0) s_np = np;
+    }
+    __syncthreads();
+    const int np = s_np;
+    for (int p0 = 0; p0 < np; p0 += 16) {
+      float4 xp[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) xp[q] = *reinterpret_cast<const float4 *>(Xr + (int64_t)s_pidx[p0 + q] * ld);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const double bo = s_pbo[p0 + q], bn = s_pbn[p0 + q];
+        const double a0 = xp[q].x, a1 = xp[q].y, a2 = xp[q].z, a3 = xp[q].w;
+        e0 = (e0 + a0 * bo) - a0 * bn;
+        e1 = (e1 + a1 * bo) - a1 * bn;
+        e2 = (e2 + a2 * bo) - a2 * bn;
+        e3 = (e3 + a3 * bo) - a3 * bn;
+      }
+    }
+  }
+  if (cc == 0 && w == 0 && valid) {
+    *reinterpret_cast<double2 *>(eps_out + row0) = make_double2(e0, e1);
+    *reinterpret_cast<double2 *>(eps_out + row0 + 2) = make_double2(e2, e3);
+  }
+  if (!valid) e0 = e1 = e2 = e3 = 0.0;
+  // partial dots: 4 rows per lane, then the wave transpose-reduction over the 64 lanes
+  double v[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    if (j < CW) {
+      v[j] = (((double)x[j].x * e0 + (double)x[j].y * e1) + (double)x[j].z * e2) + (double)x[j].w * e3;
+    } else {
+      v[j] = 0.0;
+    }
+  }
+  const double r = wave_reduce32(v, lane);
+  const int col = reduce32_col(lane);
+  double *slab1 = d.slab1 + par * d.slab1_stride;
+  double *slab2 = d.slab2 + par * d.slab2_stride;
+  int *cnt1 = d.cnt1 + par * (d.NG * NC);
+  if ((lane & 1) == 0 && col < CW) st_sc1(slab1 + (int64_t)rg * B + cc * CB + w * CW + col, r);
+  // level-2: last arriver of the group sums the group's partials in row-tile order
+  const int grp = rg / STREAM_GROUP;
+  const int g0 = grp * STREAM_GROUP;
+  const int gsz = min(STREAM_GROUP, d.RG - g0);
+  if (last_arriver_wt(cnt1 + grp * NC + cc, gsz, &s_last)) {
+    if (t < CB) {
+      double v16[STREAM_GROUP];
+#pragma unroll
+      for (int q = 0; q < STREAM_GROUP; ++q)
+        v16[q] = q < gsz ? ld_sc1(slab1 + (int64_t)(g0 + q) * B + cc * CB + t) : 0.0;
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < STREAM_GROUP; ++q) acc += v16[q];
+      st_sc1(slab2 + (int64_t)grp * B + cc * CB + t, acc);
+    }
+    if (t == 0) cnt1[grp * NC + cc] = 0;
+    publish_add(d.gdone + par, 1);  // k_solve(s) waits for NG * NC groups
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// k_solve(s): one workgroup.  Exact single-site updates of block position s in visit order.
+//   num_j = d_j - sum_{i changed in block s-1} C_ij delta_i + xsq_j b_j - sum_{i<j in s} G_ji delta_i
+// with d = X_s^T E_{s-1} from k_stream(s) and C the cross-Gram of the two blocks.  Waits (device
+// counter) for k_stream(s)'s reduction groups, publishes block s's changes for k_solve(s+1)
+// and k_stream(s+2).
+// LDS layout (B positions):
+//   doubles  r0, lo, hi, dsel, sdz, bo, bn, x2, p, z [B each], a [K][B], den [K-1][B]
+//   ints     fl, ks, gi, m, slot, spos [B each], misc [16]
+//   slots    nslot Gram rows (B doubles each), staged for the positions predicted to change
+enum PrFlag : int { PF_EX = 1 << 8, PF_LIKELY = 1 << 9 };
+
+__host__ __device__ inline size_t solve_fixed_bytes(int B, int K) {
+  return (size_t)(10 + K + (K > 1 ? K - 1 : 0)) * 8 * B + (size_t)6 * 4 * B + 64;
+}
+constexpr size_t SOLVE_LDS_MAX = 160 * 1024;
+
+// One block position s, by one workgroup (called per launch, or in a loop by the persistent
+// solver).  Phase A needs nothing from k_stream(s): per-position constants, the previous
+// block's changes and their cross-Gram correction.  Phase B waits for k_stream(s)'s reduction
+// groups, then decides, stages Gram rows, runs the serial chain and publishes.
+template <bool HS, int B>
+__device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, int nslot, char *smem) {
+#pragma clang fp contract(off)
+  constexpr int NPT = (B + 255) / 256;  // positions per thread, parallel phases
+  constexpr int NS = B / 64;            // positions per lane (contiguous), serial chain
+  const int K = HS ? 1 : d.K;
+  const int KD = K > 1 ? K - 1 : 0;
+  double *Lr0 = reinterpret_cast<double *>(smem);
+  double *Llo = Lr0 + B, *Lhi = Llo + B, *Ldsel = Lhi + B, *Lsdz = Ldsel + B, *Lbo = Lsdz + B, *Lbn = Lbo + B,
+         *Lx2 = Lbn + B, *Lp = Lx2 + B, *Lz = Lp + B, *La = Lz + B, *Lden = La + (int64_t)K * B;
+  int *Lfl = reinterpret_cast<int *>(Lden + (int64_t)KD * B);
+  int *Lks = Lfl + B, *Lgi = Lks + B, *Lm = Lgi + B, *Lslot = Lm + B, *Lspos = Lslot + B, *misc = Lspos + B;
+  double *slots = reinterpret_cast<double *>(misc + 16);
 
   const int t = threadIdx.x;
+  const int lane = t & 63, wv = t >> 6;
   const int bs = d.bsz[s];
   const int gb = d.gblk[s];
-  // 1) Gram block -> LDS (row-major, stride B), overlapped with the first batch of the
-  //    dot-product reduction loads (slab2 rows padded to a multiple of 32 with zeros)
-  const int tc = t < B ? t : 0;
-  double sv[32];
+  const int par = s & 1;
+  const bool prof = d.sc->prof_on;
+  uint64_t tp0 = prof ? wall_clock64() : 0, tp1 = 0, tp2 = 0, tp3 = 0, tw = 0;
+  const double sigmaE = d.sc->sigmaE;
+  const int64_t S = d.nbB;
+  const int64_t q0 = (int64_t)s * B;
+  const int NC = B >= 128 ? B / 128 : 1;
+
+  // A) everything that does not depend on k_stream(s)
+  const double *C = nullptr;
+  int np_prev = 0;
+  const int *pv_gi = nullptr;
+  const double *pv_bo = nullptr, *pv_bn = nullptr;
+  if (s > 0) {  // cross-Gram rows of the previous block (cycle neighbours)
+    const int gp = d.gblk[s - 1];
+    C = (gb == (gp + 1) % d.nb) ? d.xgram + (int64_t)gp * B * B : d.xgramT + (int64_t)gb * B * B;
+    const int slot = (s - 1) % 3;
+    np_prev = ld_sc1_int(d.pend_n + slot);  // written with sc1 stores by the previous block
+    pv_gi = d.pend_gi + slot * d.pend_stride;
+    pv_bo = d.pend_bo + slot * d.pend_stride;
+    pv_bn = d.pend_bn + slot * d.pend_stride;
+  }
 #pragma unroll
-  for (int q = 0; q < 32; ++q) sv[q] = d.slab2[(int64_t)q * B + tc];
+  for (int c = 0; c < NPT; ++c) {
+    const int pos = t + 256 * c;
+    if (pos < bs) {
+      const int64_t q = q0 + pos;
+      const int gi = d.gidx[q];
+      double av[MAXK], dv[MAXK];
+#pragma unroll
+      for (int k = 0; k < MAXK; ++k) {
+        av[k] = k < K ? d.mc[(MC_A + k) * S + q] : 0.0;
+        dv[k] = k < KD ? d.mc[(MC_A + K + k) * S + q] : 0.0;
+      }
+      const double bo = d.mc[MC_BO * S + q];
+      Lbo[pos] = bo;
+      Lbn[pos] = bo;
+      Lx2[pos] = d.mc[MC_XSQ * S + q];
+      Lp[pos] = HS ? 0.0 : d.mc[MC_P * S + q];
+      Lz[pos] = d.mc[MC_Z * S + q];
+      Lm[pos] = d.member[q];
+      Lgi[pos] = gi;
+#pragma unroll
+      for (int k = 0; k < MAXK; ++k) {
+        if (k < K) La[k * B + pos] = av[k];
+        if (k < KD) Lden[k * B + pos] = dv[k];
+      }
+      // sum_i (x_j . x_i) delta_i over block s-1's changes (list order)
+      double corr = 0.0;
+      for (int i0 = 0; i0 < np_prev; i0 += 8) {
+        double cv[8], dl[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          cv[u] = C[(int64_t)ld_sc1_int(pv_gi + i0 + u) * B + gi];
+          dl[u] = ld_sc1(pv_bn + i0 + u) - ld_sc1(pv_bo + i0 + u);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) corr += cv[u] * dl[u];
+      }
+      Lr0[pos] = corr;
+    }
+  }
+  // B) wait for k_stream(s)'s reduction groups (other queue), then re-arm the counter (the
+  //    next writer, k_stream(s+2), cannot start its reduction before this block publishes)
+  if (t == 0) {
+    wait_geq(d.gdone + par, d.NG * NC, &d.sc->err);
+    __hip_atomic_store(d.gdone + par, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (prof) tw = wall_clock64();
+  const double *slab2 = d.slab2 + par * d.slab2_stride;
+  // 1) num at the block start, decisions with their windows; Gram-row slots for the positions
+  //    predicted to change (position order)
+  int base = 0;
+#pragma unroll
+  for (int c = 0; c < NPT; ++c) {
+    const int pos = t + 256 * c;
+    bool likely = false;
+    if (pos < bs) {
+      double dsum = 0.0;
+      for (int g0 = 0; g0 < d.NG; g0 += 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = g0 + u < d.NG ? ld_sc1(slab2 + (int64_t)(g0 + u) * B + pos) : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) dsum += v[u];
+      }
+      const double bo = Lbo[pos], x2 = Lx2[pos];
+      // num = x.(eps + x b_old) (BayesRv2.cpp:191-193), x.eps = d - cross-Gram correction
+      const double r = (dsum - Lr0[pos]) + x2 * bo;
+      FastDec o;
+      double dsel;
+      if (HS) {
+        o.k = 1; o.lo = -1e308; o.hi = 1e308; o.ex = false;
+        dsel = La[pos];  // D (HorseshoeR.cpp:232-234)
+        likely = true;
+      } else {
+        o = decide_pos(d, r, La + pos, Lden + pos, B, sigmaE, Lp[pos], x2, Lm[pos]);
+        dsel = (!o.ex && o.k >= 1 && o.k != FALLTHROUGH) ? Lden[(o.k - 1) * B + pos] : 1.0;
+        likely = o.ex || !(o.k == FALLTHROUGH || (o.k == 0 && bo == 0.0));
+      }
+      Lfl[pos] = (o.k & 0xFF) | (o.ex ? PF_EX : 0) | (likely ? PF_LIKELY : 0);
+      Lks[pos] = o.k & 0xFF;
+      Lr0[pos] = r;
+      Llo[pos] = o.lo;
+      Lhi[pos] = o.hi;
+      Ldsel[pos] = dsel;
+      Lsdz[pos] = sqrt(sigmaE / dsel) * Lz[pos];  // rnorm(muk, sqrt(sigmaE/denom)) noise
+    }
+    const uint64_t bal = __ballot(likely);
+    if (lane == 0) misc[wv] = __popcll(bal);
+    __syncthreads();
+    int pre = base;
+    for (int w = 0; w < wv; ++w) pre += misc[w];
+    if (pos < bs) {
+      const int idx = pre + __popcll(bal & ((1ull << lane) - 1ull));
+      const int sl = likely && idx < nslot ? idx : -1;
+      Lslot[pos] = sl;
+      if (sl >= 0) Lspos[sl] = pos;
+    }
+    base += misc[0] + misc[1] + misc[2] + misc[3];
+    __syncthreads();
+  }
+  const int nused = min(base, nslot);
+  if (prof) tp1 = wall_clock64();
+  // 2) stage the predicted positions' Gram rows (8 double2 loads in flight per thread)
   {
-    const double2 *src = reinterpret_cast<const double2 *>(d.gram + (int64_t)gb * B * B) + t;
-    double2 *dst = reinterpret_cast<double2 *>(Gl) + t;
-    constexpr int NQ = B * B / 2 / 256;
-    double2 tmp[NQ];
+    const double2 *G2 = reinterpret_cast<const double2 *>(d.gram + (int64_t)gb * B * B);
+    double2 *S2 = reinterpret_cast<double2 *>(slots);
+    constexpr int H = B / 2;
+    const int tot = nused * H;
+    for (int e0 = 0; e0 < tot; e0 += 256 * 8) {
+      double2 v[8];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) tmp[q] = src[q * 256];
+      for (int u = 0; u < 8; ++u) {
+        const int e = min(e0 + u * 256 + t, tot - 1);
+        v[u] = G2[(int64_t)Lgi[Lspos[e / H]] * H + (e % H)];
+      }
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) dst[q * 256] = tmp[q];
-  }
-  double dsum = 0.0;
-#pragma unroll
-  for (int q = 0; q < 32; ++q) dsum += sv[q];
-  for (int q0 = 32; q0 < d.NG; q0 += 32) {
-#pragma unroll
-    for (int q = 0; q < 32; ++q) sv[q] = d.slab2[(int64_t)(q0 + q) * B + tc];
-#pragma unroll
-    for (int q = 0; q < 32; ++q) dsum += sv[q];
-  }
-  // 2) per-marker preparation, one thread per position
-  const Scal sc = *d.sc;
-  if (t < bs) {
-    const int m = d.member[(int64_t)s * B + t];
-    const int64_t gm = d.col_offset + m;
-    const double bo = d.beta[m];
-    const double x2 = d.xsq[m];
-    const double r = dsum + x2 * bo;  // num = x.(eps + x b_old)
-    const double p = uniform(d.seed, T_MARKER, (uint32_t)gm, it, 0);
-    const double z = normal(d.seed, T_MARKER, (uint32_t)gm, it, 1);
-    const int g = (d.gAssign && !HS) ? d.gAssign[m] : 0;
-    mrk[t] = m;
-    gi[t] = d.gidx[(int64_t)s * B + t];
-    grp[t] = g;
-    bold[t] = bo;
-    xq[t] = x2;
-    pz[t] = z;
-    pu[t] = p;
-    r_[t] = r;
-    if (HS) {
-      const double lam = d.lambda[m];
-      const double sv = sc.tau * sc.c2 * lam / (sc.tau * lam + sc.c2);
-      const double D = x2 + (sc.sigmaE / sv);
-      ide[t] = 1.0 / D;
-      sdz[t] = sqrt(sc.sigmaE / D) * z;  // HorseshoeR.cpp:234
-      k0[t] = 1;
-      tlo[t] = 0.0;
-      thi[t] = 1e308;
-    } else {
-      Decision dc = decide_bayesr(r, x2, sc.sigmaE, d.sigmaGG[g], d.pi + (int64_t)g * d.K,
-                                  d.cva + g, d.G, d.K, p, true);
-      k0[t] = dc.k;
-      ide[t] = 1.0 / dc.denom;
-      sdz[t] = sqrt(sc.sigmaE / dc.denom) * z;  // BayesRv2.cpp:228
-      const double t0 = r * r;
-      tlo[t] = t0 - dc.margin;
-      thi[t] = dc.margin > 0.0 ? t0 + dc.margin : -1.0;  // empty interval -> slow path
+      for (int u = 0; u < 8; ++u)
+        if (e0 + u * 256 + t < tot) S2[e0 + u * 256 + t] = v[u];
     }
   }
   __syncthreads();
-  // 3) serial chain on wave 0 (lane l owns positions l + 64 q).  A ballot finds the next
-  //    position whose update may change beta (fast decision changes it, or its corrected num^2
-  //    left the invariant window); runs of unchanged positions are committed in one step.  The
-  //    owner's new beta is broadcast by readlane and every later position subtracts G_ji*delta.
+  if (prof) tp2 = wall_clock64();
+  // 3) serial chain on wave 0; lane l owns positions l*NS .. l*NS+NS-1.  Per position: the
+  //    current num (r), its decision window [lo, hi] in num^2, and two bits: act (the decision
+  //    changes beta, or needs the exact formula) and win (num^2 inside the window).  The next
+  //    position to visit is the lowest one with act or !win; runs of unchanged positions in
+  //    between are committed as they are.  A position found outside its window is re-decided
+  //    at its current num (wave-uniform) and re-examined.  A visited position's new beta is
+  //    computed wave-uniformly and every later position subtracts G_ji * delta.
   if (t < 64) {
-    const int lane = t;
-    constexpr int NS = B / 64;
-    double r[NS], lo[NS], hi[NS], id[NS], sz[NS], bo[NS], bf[NS];
-    int kk[NS], gg[NS], kf[NS];
+    double r[NS], lo[NS], hi[NS];
+    int gg[NS];
+    uint32_t act = 0, win = 0, valid = 0;
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
-      const int pos = q * 64 + lane;
+      const int pos = lane * NS + q;
       const bool in = pos < bs;
-      r[q] = in ? r_[pos] : 0.0;
-      lo[q] = in ? tlo[pos] : 0.0;
-      hi[q] = in ? thi[pos] : -1.0;
-      id[q] = in ? ide[pos] : 0.0;
-      sz[q] = in ? sdz[pos] : 0.0;
-      bo[q] = in ? bold[pos] : 0.0;
-      kk[q] = in ? k0[pos] : 0;
-      gg[q] = in ? gi[pos] : 0;
-      bf[q] = bo[q];
-      kf[q] = kk[q];
+      r[q] = in ? Lr0[pos] : 0.0;
+      lo[q] = in ? Llo[pos] : 1.0;
+      hi[q] = in ? Lhi[pos] : -1.0;
+      gg[q] = in ? Lgi[pos] : 0;
+      const int fl = in ? Lfl[pos] : 0;
+      const double tt = r[q] * r[q];
+      valid |= (uint32_t)in << q;
+      act |= (uint32_t)(in && (HS || (fl & PF_LIKELY))) << q;
+      win |= (uint32_t)(in && tt >= lo[q] && tt <= hi[q]) << q;
     }
-    int nslow = 0;
+    constexpr uint32_t ALL = NS >= 32 ? 0xFFFFFFFFu : ((1u << NS) - 1u);
+    const double *Ggl = d.gram + (int64_t)gb * B * B;
+    int nslow = 0, nsteps = 0, nref = 0, nglob = 0;
+    uint64_t tref = 0, tcor = 0;
     int i = 0;
     while (i < bs) {
-      int first = bs;
-#pragma unroll
-      for (int q = NS - 1; q >= 0; --q) {
-        const int pos = q * 64 + lane;
-        const double tt = r[q] * r[q];
-        const bool fast = tt >= lo[q] && tt <= hi[q];
-        const bool nochange = !HS && fast && (kk[q] == FALLTHROUGH || (kk[q] == 0 && bo[q] == 0.0));
-        const uint64_t bal = __ballot(pos >= i && pos < bs && !nochange);
-        if (bal) first = q * 64 + __builtin_ctzll(bal);
-      }
-      if (first >= bs) break;  // the rest keep their fast decisions (no change)
-      const int qs = first >> 6, l = first & 63;  // wave-uniform
-      double rv = r[0], lov = lo[0], hiv = hi[0], idv = id[0], szv = sz[0], bov = bo[0];
-      int kv = kk[0], gv = gg[0];
+      const int lowq = min(max(i - lane * NS, 0), NS);
+      const uint32_t ge = ALL & ~((1u << lowq) - 1u);
+      const uint32_t cand = valid & (act | ~win) & ge;
+      const uint64_t bal = __ballot(cand != 0);
+      if (!bal) break;  // the rest keep their decisions (no change)
+      const int L = __builtin_ctzll(bal);
+      const uint32_t cL = (uint32_t)__builtin_amdgcn_readlane((int)cand, L);
+      const int qf = __builtin_ctz(cL);
+      const int first = L * NS + qf;  // wave-uniform
+      double rv = r[0];
 #pragma unroll
       for (int q = 1; q < NS; ++q)
-        if (qs == q) { rv = r[q]; lov = lo[q]; hiv = hi[q]; idv = id[q]; szv = sz[q]; bov = bo[q]; kv = kk[q]; gv = gg[q]; }
+        if (qf == q) rv = r[q];
+      const double rf = readlane_f64(rv, L);
+      const int fl = Lfl[first];
+      const bool exf = (fl & PF_EX) != 0;
+      const bool winf = ((uint32_t)__builtin_amdgcn_readlane((int)win, L) >> qf) & 1u;
+      if (!HS && !exf && !winf) {
+        // re-decide `first` at its current num (wave-uniform), then re-examine it
+        const uint64_t tr0 = prof ? wall_clock64() : 0;
+        FastDec o = decide_pos(d, rf, La + first, Lden + first, B, sigmaE, Lp[first], Lx2[first], Lm[first]);
+        const double bo = Lbo[first];
+        const bool lk = o.ex || !(o.k == FALLTHROUGH || (o.k == 0 && bo == 0.0));
+        const double dsel = (!o.ex && o.k >= 1 && o.k != FALLTHROUGH) ? Lden[(o.k - 1) * B + first] : 1.0;
+        if (lane == 0) {
+          Lfl[first] = (o.k & 0xFF) | (o.ex ? PF_EX : 0) | (lk ? PF_LIKELY : 0);
+          Lks[first] = o.k;
+          Ldsel[first] = dsel;
+          Lsdz[first] = sqrt(sigmaE / dsel) * Lz[first];
+        }
+        if (lane == L) {
+#pragma unroll
+          for (int q = 0; q < NS; ++q)
+            if (q == qf) { lo[q] = o.lo; hi[q] = o.hi; }
+          act = (act & ~(1u << qf)) | ((uint32_t)lk << qf);
+          win = (win & ~(1u << qf)) | ((uint32_t)(!o.ex) << qf);
+        }
+        ++nref;
+        if (prof) tref += wall_clock64() - tr0;
+        continue;
+      }
+      const double bof = Lbo[first];
       double bn;
       int ks;
       if (HS) {
-        bn = rv * idv + szv;
+        bn = rf / Ldsel[first] + Lsdz[first];  // HorseshoeR.cpp:234
         ks = 1;
+      } else if (exf) {
+        const int m = Lm[first];
+        const int g = d.gAssign ? d.gAssign[m] : 0;
+        Decision dc = decide_bayesr(rf, Lx2[first], sigmaE, d.sigmaGG[g], d.pi + (int64_t)g * d.K, d.cva + g, d.G,
+                                    d.K, Lp[first], false);
+        ks = dc.k;
+        bn = dc.k == 0 ? 0.0 : (dc.k == FALLTHROUGH ? bof : rf / dc.denom + sqrt(sigmaE / dc.denom) * Lz[first]);
+        ++nslow;
       } else {
-        const double tt = rv * rv;
-        const int fast = __builtin_amdgcn_readlane((int)(tt >= lov && tt <= hiv), l);
-        if (fast) {
-          ks = kv;
-          bn = kv == 0 ? 0.0 : (kv == FALLTHROUGH ? bov : rv * idv + szv);
-        } else {
-          const double ri = readlane_f64(rv, l);  // uniform inputs -> uniform result
-          const double boi = readlane_f64(bov, l);
-          ks = chain_slow(d, ri, xq[first], grp[first], pu[first], pz[first], sc.sigmaE, &bn, boi);
-          ++nslow;
-        }
+        ks = fl & 0xFF;
+        bn = ks == 0 ? 0.0 : (ks == FALLTHROUGH ? bof : rf / Ldsel[first] + Lsdz[first]);  // BayesRv2.cpp:226-230
       }
-      const double delta = readlane_f64(bn - bov, l);
-      const int ksu = __builtin_amdgcn_readlane(ks, l);
-      const int gf = __builtin_amdgcn_readlane(gv, l);
-      const double *grow = Gl + gf * B;
+      if (lane == 0) { Lbn[first] = bn; Lks[first] = ks; }
+      const double delta = bn - bof;
+      if (delta != 0.0) {
+        const uint64_t tc0 = prof ? wall_clock64() : 0;
+        const int sl = Lslot[first];
+        nglob += sl < 0;
+        const double *grow = sl >= 0 ? slots + (int64_t)sl * B : Ggl + (int64_t)Lgi[first] * B;
+        uint32_t w2 = win;
 #pragma unroll
-      for (int q = 0; q < NS; ++q) {
-        const int pos = q * 64 + lane;
-        if (pos == first) { bf[q] = bn; kf[q] = ksu; }
-        if (pos > first && delta != 0.0) r[q] = r[q] - grow[gg[q]] * delta;
+        for (int q = 0; q < NS; ++q) {
+          const int pos = lane * NS + q;
+          if (pos > first && pos < bs) {
+            r[q] = r[q] - grow[gg[q]] * delta;
+            const double tt = r[q] * r[q];
+            const uint32_t b = (uint32_t)(tt >= lo[q] && tt <= hi[q]);
+            w2 = (w2 & ~(1u << q)) | (b << q);
+          }
+        }
+        win = w2;
+        if (prof) tcor += wall_clock64() - tc0;
       }
       i = first + 1;
-    }
-#pragma unroll
-    for (int q = 0; q < NS; ++q) {
-      const int pos = q * 64 + lane;
-      if (pos < bs) { ksel[pos] = kf[q]; bnw[pos] = bf[q]; }
+      ++nsteps;
     }
     if (lane == 0 && nslow) atomicAdd(&d.sc->n_slow, (unsigned long long)nslow);
-  }
-  __syncthreads();
-  // 4) write back, compact the changed markers into the pending list (position order)
-  int changed = 0;
-  if (t < bs) {
-    const int m = mrk[t];
-    const int ks = ksel[t];
-    d.beta[m] = bnw[t];
-    if (!HS) {
-      if (ks != FALLTHROUGH) d.comp[m] = ks;
-      d.sel[m] = ks != FALLTHROUGH;
+    if (prof && lane == 0) {
+      atomicAdd(&d.sc->prof[6], (unsigned long long)nsteps);
+      atomicAdd(&d.sc->prof[7], (unsigned long long)nref);
+      atomicAdd(&d.sc->prof[4], (unsigned long long)nglob);
+      atomicAdd(&d.sc->prof[8], (unsigned long long)tref);
+      atomicAdd(&d.sc->prof[9], (unsigned long long)tcor);
     }
-    changed = bnw[t] != bold[t];
   }
-  const uint64_t bal = __ballot(changed);
-  const int lane = t & 63, wv = t >> 6;
-  if (lane == 0) misc[wv] = __popcll(bal);
   __syncthreads();
-  int base = 0;
-  for (int q = 0; q < wv; ++q) base += misc[q];
-  if (changed) {
-    const int idx = base + __popcll(bal & ((1ull << lane) - 1ull));
-    d.pend_idx[idx] = mrk[t];
-    d.pend_bo[idx] = bold[t];
-    d.pend_bn[idx] = bnw[t];
+  if (prof) tp3 = wall_clock64();
+  // 4) write back, compact the changed markers into this block's list (position order)
+  const int pslot = s % 3;
+  int *pidx = d.pend_idx + pslot * d.pend_stride, *pgi = d.pend_gi + pslot * d.pend_stride;
+  double *pbo = d.pend_bo + pslot * d.pend_stride, *pbn = d.pend_bn + pslot * d.pend_stride;
+  base = 0;
+#pragma unroll
+  for (int c = 0; c < NPT; ++c) {
+    const int pos = t + 256 * c;
+    int changed = 0;
+    double bnv = 0.0, bov = 0.0;
+    int m = 0;
+    if (pos < bs) {
+      m = Lm[pos];
+      const int ks = Lks[pos];
+      bnv = Lbn[pos];
+      bov = Lbo[pos];
+      d.beta[m] = bnv;
+      if (!HS) {
+        if (ks != FALLTHROUGH) d.comp[m] = ks;
+        d.sel[m] = ks != FALLTHROUGH;
+      }
+      changed = bnv != bov;
+    }
+    const uint64_t bal = __ballot(changed);
+    if (lane == 0) misc[wv] = __popcll(bal);
+    __syncthreads();
+    int pre = base;
+    for (int w = 0; w < wv; ++w) pre += misc[w];
+    if (changed) {
+      const int idx = pre + __popcll(bal & ((1ull << lane) - 1ull));
+      st_sc1_int(pidx + idx, m);
+      st_sc1_int(pgi + idx, Lgi[pos]);
+      st_sc1(pbo + idx, bov);
+      st_sc1(pbn + idx, bnv);
+    }
+    base += misc[0] + misc[1] + misc[2] + misc[3];
+    __syncthreads();
   }
-  const int npend = misc[0] + misc[1] + misc[2] + misc[3];
-  const int npad = (npend + 31) & ~31;  // k_stream reads the list in batches of 32
-  if (t >= npend && t < npad) {  // neutral padding: eps + x*0 - x*0 == eps exactly
-    d.pend_idx[t] = 0;
-    d.pend_bo[t] = 0.0;
-    d.pend_bn[t] = 0.0;
+  const int npend = base;
+  const int npad = (npend + 15) & ~15;  // lists are read in batches of 8 / 16
+  if (npend + t < npad) {  // neutral padding: eps + x*0 - x*0 == eps exactly, delta = 0
+    st_sc1_int(pidx + npend + t, 0);
+    st_sc1_int(pgi + npend + t, 0);
+    st_sc1(pbo + npend + t, 0.0);
+    st_sc1(pbn + npend + t, 0.0);
   }
+  if (t == 0) st_sc1_int(d.pend_n + pslot, npad);
+  // publish: every storing wave drains its sc1 stores, then the block count (k_stream(s+2))
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   if (t == 0) {
-    d.sc->n_pend = npad;
+    __hip_atomic_store(&d.sc->pend_seq, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (npend) atomicAdd(&d.sc->n_changed, (unsigned long long)npend);
+    if (prof) {
+      const uint64_t tp4 = wall_clock64();
+      atomicAdd(&d.sc->prof[0], (unsigned long long)(tp1 - tw));
+      atomicAdd(&d.sc->prof[1], (unsigned long long)(tp2 - tp1));
+      atomicAdd(&d.sc->prof[2], (unsigned long long)(tp3 - tp2));
+      atomicAdd(&d.sc->prof[3], (unsigned long long)(tp4 - tp3));
+      atomicAdd(&d.sc->prof[5], 1ull);
+      atomicAdd(&d.sc->prof[10], (unsigned long long)(tw - tp0));
+    }
+  }
+}
+
+template <bool HS, int B>
+__global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it, int nslot) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  solve_block<HS, B>(d, s, it, nslot, smem);
+}
+
+// Persistent solver: one launch per sweep on the solve queue's reserved CU, looping over the
+// block positions; each iteration's phase A (prefetch) overlaps the wait for k_stream(s).
+template <bool HS, int B>
+__global__ __launch_bounds__(256) void k_solve_sweep(Dev d, uint32_t it, int nslot) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  for (int s = 0; s < d.nb; ++s) {
+    solve_block<HS, B>(d, s, it, nslot, smem);
+    __syncthreads();
   }
 }
 
@@ -889,10 +1287,22 @@ __global__ __launch_bounds__(256) void k_markers(Dev d, int mode, uint32_t it) {
   }
   for (int q = threadIdx.x; q < d.G * d.K; q += 256) out[2 + d.G + q] = (double)cnt[q];
   if (last_arriver(d.mcnt, gridDim.x, &s_last)) {
-    for (int q = threadIdx.x; q < NS; q += 256) {
-      double acc = 0.0;
-      for (int w = 0; w < (int)gridDim.x; ++w) acc += d.mslab[(int64_t)w * NS + q];
-      d.stats[q] = acc;
+    const int nw = (int)gridDim.x;
+    if (NS <= 64) {
+      // wave per statistic, lanes stride over the workgroup slabs (fixed order), wave tree
+      const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+      for (int q = wv; q < NS; q += 4) {
+        double acc = 0.0;
+        for (int w = lane; w < nw; w += 64) acc += d.mslab[(int64_t)w * NS + q];
+        acc = wave_sum(acc);
+        if (lane == 0) d.stats[q] = acc;
+      }
+    } else {
+      for (int q = threadIdx.x; q < NS; q += 256) {
+        double acc = 0.0;
+        for (int w = 0; w < nw; ++w) acc += d.mslab[(int64_t)w * NS + q];
+        d.stats[q] = acc;
+      }
     }
     if (threadIdx.x == 0) *d.mcnt = 0;
   }
@@ -1025,10 +1435,10 @@ hipError_t launch_cast_x(const void *src, bool is_f64, int64_t lds, float *dst, 
   return hipGetLastError();
 }
 
-hipError_t launch_gram(const Dev &d, int nblocks, hipStream_t st) {
+hipError_t launch_gram(const Dev &d, int shift, double *G, double *GT, hipStream_t st) {
   const int nt = (d.B + 63) / 64;
-  hipLaunchKernelGGL(k_gram, dim3((unsigned)nblocks, (unsigned)(nt * nt)), dim3(256), 0, st, d.X, d.ld,
-                     d.member, d.bsz, d.B, d.gram);
+  hipLaunchKernelGGL(k_gram, dim3((unsigned)d.nb, (unsigned)(nt * nt)), dim3(256), 0, st, d.X, d.ld, d.member,
+                     d.bsz, d.B, d.nb, shift, G, GT);
   return hipGetLastError();
 }
 
@@ -1038,8 +1448,9 @@ hipError_t launch_xsq(const Dev &d, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_rows(const Dev &d, int flags, const double *deps_in, hipStream_t st) {
-  hipLaunchKernelGGL(k_rows, dim3(cdiv64(d.N, 256)), dim3(256), 0, st, d, flags, deps_in);
+hipError_t launch_rows(const Dev &d, int flags, const double *deps_in, hipStream_t st, const double *eps_in,
+                       int slot_a, int slot_b) {
+  hipLaunchKernelGGL(k_rows, dim3(cdiv64(d.N, 256)), dim3(256), 0, st, d, flags, deps_in, eps_in, slot_a, slot_b);
   return hipGetLastError();
 }
 
@@ -1049,10 +1460,7 @@ hipError_t launch_sweep_start(const Dev &d, uint32_t it, hipStream_t st) {
 }
 
 hipError_t launch_perm(const Dev &d, uint32_t it, int shard, bool identity, hipStream_t st) {
-  if (!identity) {
-    const size_t lds = d.nb <= PERM_LDS_MAX ? sizeof(int) * (size_t)d.nb : 0;
-    hipLaunchKernelGGL(k_perm_blockorder, dim3(1), dim3(256), lds, st, d, it, shard);
-  }
+  hipLaunchKernelGGL(k_perm_blockorder, dim3(1), dim3(256), 0, st, d, it, shard, identity ? 1 : 0);
   hipLaunchKernelGGL(k_perm_within, dim3((unsigned)d.nb), dim3(64), 0, st, d, it, identity ? 1 : 0);
   return hipGetLastError();
 }
@@ -1062,42 +1470,90 @@ hipError_t launch_fixed(const Dev &d, uint32_t it, bool perm_on_device, hipStrea
   return hipGetLastError();
 }
 
-hipError_t launch_stream(const Dev &d, int s, hipStream_t st) {
-  if (d.B == 64)
-    hipLaunchKernelGGL(k_stream<64>, dim3((unsigned)d.RG), dim3(256), 0, st, d, s);
+hipError_t launch_stream(const Dev &d, int s, const double *eps_in, double *eps_out, hipStream_t st) {
+  const int cw = d.B >= 128 ? 32 : 16;
+  const unsigned grid = (unsigned)(((d.RG + 7) / 8) * 8 * (d.B / (4 * cw)));
+  if (cw == 32)
+    hipLaunchKernelGGL(k_stream<32>, dim3(grid), dim3(256), 0, st, d, s, eps_in, eps_out);
   else
-    hipLaunchKernelGGL(k_stream<128>, dim3((unsigned)d.RG), dim3(256), 0, st, d, s);
+    hipLaunchKernelGGL(k_stream<16>, dim3(grid), dim3(256), 0, st, d, s, eps_in, eps_out);
   return hipGetLastError();
 }
 
-size_t solve_lds_bytes(int B) { return (size_t)B * B * 8 + (size_t)B * 10 * 8 + (size_t)B * 5 * 4 + 64; }
+hipError_t launch_prep(const Dev &d, uint32_t it, hipStream_t st) {
+  const unsigned grid = cdiv64(d.nbB, 256);
+  if (d.model == MODEL_HORSESHOE)
+    hipLaunchKernelGGL(k_prep<true>, dim3(grid), dim3(256), 0, st, d, it);
+  else
+    hipLaunchKernelGGL(k_prep<false>, dim3(grid), dim3(256), 0, st, d, it);
+  return hipGetLastError();
+}
+
+// Gram-row slots that fit next to the per-position arrays (all rows when possible)
+static int solve_slots(int B, int K) {
+  const size_t fixed = solve_fixed_bytes(B, K);
+  const int n = (int)((SOLVE_LDS_MAX - fixed) / (8 * (size_t)B));
+  return n < B ? n : B;
+}
+
+size_t solve_lds_bytes(int B, int K) { return solve_fixed_bytes(B, K) + (size_t)solve_slots(B, K) * 8 * B; }
+
+template <bool HS>
+static void launch_solve_b(const Dev &d, int s, uint32_t it, hipStream_t st) {
+  const int K = HS ? 1 : d.K;
+  const int ns = solve_slots(d.B, K);
+  const size_t lds = solve_lds_bytes(d.B, K);
+  switch (d.B) {
+    case 64: hipLaunchKernelGGL((k_solve<HS, 64>), dim3(1), dim3(256), lds, st, d, s, it, ns); break;
+    case 128: hipLaunchKernelGGL((k_solve<HS, 128>), dim3(1), dim3(256), lds, st, d, s, it, ns); break;
+    case 256: hipLaunchKernelGGL((k_solve<HS, 256>), dim3(1), dim3(256), lds, st, d, s, it, ns); break;
+    default: hipLaunchKernelGGL((k_solve<HS, 512>), dim3(1), dim3(256), lds, st, d, s, it, ns); break;
+  }
+}
+
+template <bool HS>
+static void launch_solve_sweep_b(const Dev &d, uint32_t it, hipStream_t st) {
+  const int K = HS ? 1 : d.K;
+  const int ns = solve_slots(d.B, K);
+  const size_t lds = solve_lds_bytes(d.B, K);
+  switch (d.B) {
+    case 64: hipLaunchKernelGGL((k_solve_sweep<HS, 64>), dim3(1), dim3(256), lds, st, d, it, ns); break;
+    case 128: hipLaunchKernelGGL((k_solve_sweep<HS, 128>), dim3(1), dim3(256), lds, st, d, it, ns); break;
+    case 256: hipLaunchKernelGGL((k_solve_sweep<HS, 256>), dim3(1), dim3(256), lds, st, d, it, ns); break;
+    default: hipLaunchKernelGGL((k_solve_sweep<HS, 512>), dim3(1), dim3(256), lds, st, d, it, ns); break;
+  }
+}
+
+hipError_t launch_solve_sweep(const Dev &d, uint32_t it, hipStream_t st) {
+  if (d.model == MODEL_HORSESHOE) launch_solve_sweep_b<true>(d, it, st);
+  else launch_solve_sweep_b<false>(d, it, st);
+  return hipGetLastError();
+}
 
 hipError_t launch_solve(const Dev &d, int s, uint32_t it, hipStream_t st) {
-  const size_t lds = solve_lds_bytes(d.B);
-  const bool hs = d.model == MODEL_HORSESHOE;
-  if (d.B == 64) {
-    if (hs) hipLaunchKernelGGL((k_solve<true, 64>), dim3(1), dim3(256), lds, st, d, s, it);
-    else hipLaunchKernelGGL((k_solve<false, 64>), dim3(1), dim3(256), lds, st, d, s, it);
-  } else {
-    if (hs) hipLaunchKernelGGL((k_solve<true, 128>), dim3(1), dim3(256), lds, st, d, s, it);
-    else hipLaunchKernelGGL((k_solve<false, 128>), dim3(1), dim3(256), lds, st, d, s, it);
-  }
+  if (d.model == MODEL_HORSESHOE) launch_solve_b<true>(d, s, it, st);
+  else launch_solve_b<false>(d, s, it, st);
   return hipGetLastError();
 }
 
 hipError_t set_solve_lds_limit(int /*B*/) {
-  // One limit for every variant, the largest any block size needs: lowering it for one
+  // One limit for every variant, the largest any configuration uses: lowering it for one
   // session silently shrank the LDS window of later launches (out-of-range LDS writes are
   // dropped, no fault).
-  const int lds = (int)solve_lds_bytes(BMAX);
-  const void *fns[4] = {(const void *)k_solve<true, 64>, (const void *)k_solve<false, 64>,
-                        (const void *)k_solve<true, 128>, (const void *)k_solve<false, 128>};
+  const int lds = (int)SOLVE_LDS_MAX;
+  const void *fns[16] = {(const void *)k_solve<true, 64>, (const void *)k_solve<false, 64>,
+                         (const void *)k_solve<true, 128>, (const void *)k_solve<false, 128>,
+                         (const void *)k_solve<true, 256>, (const void *)k_solve<false, 256>,
+                         (const void *)k_solve<true, 512>, (const void *)k_solve<false, 512>,
+                         (const void *)k_solve_sweep<true, 64>, (const void *)k_solve_sweep<false, 64>,
+                         (const void *)k_solve_sweep<true, 128>, (const void *)k_solve_sweep<false, 128>,
+                         (const void *)k_solve_sweep<true, 256>, (const void *)k_solve_sweep<false, 256>,
+                         (const void *)k_solve_sweep<true, 512>, (const void *)k_solve_sweep<false, 512>};
   for (const void *f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
   }
-  return hipFuncSetAttribute((const void *)k_perm_blockorder, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)(sizeof(int) * PERM_LDS_MAX));
+  return hipSuccess;
 }
 
 hipError_t launch_markers(const Dev &d, int mode, uint32_t it, hipStream_t st) {

@@ -18,16 +18,19 @@ hipError_t launch_synth_y(const float *X, int64_t ld, int64_t N, const int *cidx
                           int nc, double *y, hipStream_t st);
 hipError_t launch_cast_x(const void *src, bool is_f64, int64_t lds, float *dst, int64_t ldd,
                          int64_t N, int64_t M, hipStream_t st);
-hipError_t launch_gram(const Dev &d, int nblocks, hipStream_t st);
+hipError_t launch_gram(const Dev &d, int shift, double *G, double *GT, hipStream_t st);
 hipError_t launch_xsq(const Dev &d, hipStream_t st);
-hipError_t launch_rows(const Dev &d, int flags, const double *deps_in, hipStream_t st);
+hipError_t launch_rows(const Dev &d, int flags, const double *deps_in, hipStream_t st,
+                       const double *eps_in = nullptr, int slot_a = -1, int slot_b = -1);
 hipError_t launch_sweep_start(const Dev &d, uint32_t it, hipStream_t st);
 hipError_t launch_perm(const Dev &d, uint32_t it, int shard, bool identity, hipStream_t st);
 hipError_t launch_fixed(const Dev &d, uint32_t it, bool perm_on_device, hipStream_t st);
-hipError_t launch_stream(const Dev &d, int s, hipStream_t st);
+hipError_t launch_stream(const Dev &d, int s, const double *eps_in, double *eps_out, hipStream_t st);
+hipError_t launch_prep(const Dev &d, uint32_t it, hipStream_t st);
 hipError_t launch_solve(const Dev &d, int s, uint32_t it, hipStream_t st);
+hipError_t launch_solve_sweep(const Dev &d, uint32_t it, hipStream_t st);
 hipError_t set_solve_lds_limit(int B);
-size_t solve_lds_bytes(int B);
+size_t solve_lds_bytes(int B, int K);
 hipError_t launch_markers(const Dev &d, int mode, uint32_t it, hipStream_t st);
 hipError_t launch_hyper(const Dev &d, uint32_t it, const double *stats, hipStream_t st);
 hipError_t launch_hyper_init(const Dev &d, const double *stats, bool pi_given, hipStream_t st);

@@ -13,6 +13,7 @@
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -119,7 +120,9 @@ struct brr_session {
   Logger log;
   Dev d{};
   int device = 0;
-  hipStream_t st = nullptr;
+  hipStream_t st = nullptr;   // main queue: streaming + everything else (all CUs but one)
+  hipStream_t st2 = nullptr;  // solve queue (one reserved CU); == st when CU masks are unavailable
+  hipEvent_t ev_a = nullptr, ev_b = nullptr;  // sweep-boundary joins of the two queues
   int64_t N = 0, M = 0, M_total = 0, col_offset = 0;
   int K = 1, G = 1, F = 0, B = 128, nb = 0, model = 0, NS = 0;
   int order_mode = BRR_ORDER_BLOCKED;
@@ -139,8 +142,8 @@ struct brr_session {
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::vector<std::pair<size_t, int>> ev_pairs;  // (start index, kind 0=stream 1=solve)
-  double t_stream = 0, t_solve = 0;
-  int64_t n_stream = 0, n_solve = 0;
+  double t_stream = 0, t_solve = 0, t_solve_sweep = 0;
+  int64_t n_stream = 0, n_solve = 0, n_solve_sweep = 0;
   std::vector<void *> allocs;
 
   template <class T>
@@ -153,7 +156,11 @@ struct brr_session {
     if (st) (void)hipStreamSynchronize(st);
     if (comm) (void)ncclCommDestroy(comm);
     for (void *p : allocs) (void)hipFree(p);
+    if (st2 && st2 != st) (void)hipStreamSynchronize(st2);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
+    if (ev_a) (void)hipEventDestroy(ev_a);
+    if (ev_b) (void)hipEventDestroy(ev_b);
+    if (st2 && st2 != st) (void)hipStreamDestroy(st2);
     if (st) (void)hipStreamDestroy(st);
   }
   hipEvent_t ev() {
@@ -179,7 +186,9 @@ int collect_timing(brr_session *s) {
   for (auto &pr : s->ev_pairs) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, s->ev_pool[pr.first], s->ev_pool[pr.first + 1]));
-    if (pr.second == 0) { s->t_stream += ms; s->n_stream++; } else { s->t_solve += ms; s->n_solve++; }
+    if (pr.second == 0) { s->t_stream += ms; s->n_stream++; }
+    else if (pr.second == 1) { s->t_solve += ms; s->n_solve++; }
+    else { s->t_solve_sweep += ms; s->n_solve_sweep++; }
   }
   s->ev_pairs.clear();
   s->ev_used = 0;
@@ -203,6 +212,18 @@ int upload_order(brr_session *s, const std::vector<int32_t> &order) {
   HIPCHK(hipMemcpyAsync(s->d.bsz, bsz.data(), bsz.size() * 4, hipMemcpyHostToDevice, s->st));
   HIPCHK(hipMemcpyAsync(s->d.gblk, gb.data(), gb.size() * 4, hipMemcpyHostToDevice, s->st));
   HIPCHK(hipStreamSynchronize(s->st));  // host vectors go out of scope
+  return 0;
+}
+
+// the pipeline's bounded device waits raise sc->err instead of hanging
+int check_device_error(brr_session *s) {
+  int err = 0;
+  HIPCHK(hipStreamSynchronize(s->st));
+  HIPCHK(hipMemcpy(&err, &s->d.sc->err, sizeof err, hipMemcpyDeviceToHost));
+  if (err) {
+    set_error("device pipeline protocol timed out (k_stream / k_solve hand-over)");
+    return -3;
+  }
   return 0;
 }
 
@@ -230,7 +251,8 @@ int do_sweep_local(brr_session *s) {
     }
     s->grand.shuffle(s->ref_order);
     if (int rc = upload_order(s, s->ref_order)) return rc;
-    HIPCHK(launch_gram(d, s->nb, s->st));
+    HIPCHK(launch_gram(d, 0, d.gram, nullptr, s->st));
+    HIPCHK(launch_gram(d, 1, d.xgram, d.xgramT, s->st));
   } else {
     HIPCHK(launch_perm(d, it, s->shard, true, s->st));
   }
@@ -238,33 +260,83 @@ int do_sweep_local(brr_session *s) {
     HIPCHK(launch_fixed(d, it, s->order_mode == BRR_ORDER_BLOCKED, s->st));
   if (sharded)
     if (int rc = rows_flagged(s, H_ROW_SNAPSHOT)) return rc;
-  // the hot loop: one streaming pass + one solve per block of B markers
-  for (int b = 0; b < s->nb; ++b) {
+  // per-marker constants of the sweep in visit order
+  HIPCHK(launch_prep(d, it, s->st));
+  // the hot loop (lag-1 pipeline): k_stream(b) on the main queue overlaps k_solve(b-1) on the
+  // solve queue; the kernels hand over through device counters (pend_seq, gdone).  eps
+  // alternates between the two buffers (k_stream reads one, writes the other).  Enqueue order
+  // stream(0), stream(1), solve(0), stream(2), solve(1), ... keeps every dependency ahead in
+  // queue order, so a single queue (no CU masks) runs the same protocol without waiting.
+  const bool two = s->st2 != s->st;
+  if (two) {
+    HIPCHK(hipEventRecord(s->ev_a, s->st));
+    HIPCHK(hipStreamWaitEvent(s->st2, s->ev_a, 0));
+  }
+  double *ebuf[2] = {d.eps, d.eps2};
+  auto stream_b = [&](int b) -> int {
+    const double *ein = ebuf[b & 1];
+    double *eout = ebuf[(b + 1) & 1];
     if (s->timing) {
       const size_t i0 = s->ev_used;
       hipEvent_t e0 = s->ev(), e1 = s->ev();
       HIPCHK(hipEventRecord(e0, s->st));
-      HIPCHK(launch_stream(d, b, s->st));
+      HIPCHK(launch_stream(d, b, ein, eout, s->st));
       HIPCHK(hipEventRecord(e1, s->st));
       s->ev_pairs.push_back({i0, 0});
+    } else {
+      HIPCHK(launch_stream(d, b, ein, eout, s->st));
+    }
+    return 0;
+  };
+  auto solve_b = [&](int b) -> int {
+    if (s->timing) {
       const size_t i2 = s->ev_used;
       hipEvent_t e2 = s->ev(), e3 = s->ev();
-      HIPCHK(hipEventRecord(e2, s->st));
-      HIPCHK(launch_solve(d, b, it, s->st));
-      HIPCHK(hipEventRecord(e3, s->st));
+      HIPCHK(hipEventRecord(e2, s->st2));
+      HIPCHK(launch_solve(d, b, it, s->st2));
+      HIPCHK(hipEventRecord(e3, s->st2));
       s->ev_pairs.push_back({i2, 1});
     } else {
-      HIPCHK(launch_stream(d, b, s->st));
-      HIPCHK(launch_solve(d, b, it, s->st));
+      HIPCHK(launch_solve(d, b, it, s->st2));
     }
+    return 0;
+  };
+  if (two) {
+    // persistent solver on the reserved CU: one launch per sweep
+    if (s->timing) {
+      const size_t i2 = s->ev_used;
+      hipEvent_t e2 = s->ev(), e3 = s->ev();
+      HIPCHK(hipEventRecord(e2, s->st2));
+      HIPCHK(launch_solve_sweep(d, it, s->st2));
+      HIPCHK(hipEventRecord(e3, s->st2));
+      s->ev_pairs.push_back({i2, 2});
+    } else {
+      HIPCHK(launch_solve_sweep(d, it, s->st2));
+    }
+    for (int b = 0; b < s->nb; ++b)
+      if (int rc = stream_b(b)) return rc;
+  } else {
+    for (int b = 0; b < s->nb; ++b) {
+      if (int rc = stream_b(b)) return rc;
+      if (b >= 1)
+        if (int rc = solve_b(b - 1)) return rc;
+    }
+    if (int rc = solve_b(s->nb - 1)) return rc;
   }
+  if (two) {
+    HIPCHK(hipEventRecord(s->ev_b, s->st2));
+    HIPCHK(hipStreamWaitEvent(s->st, s->ev_b, 0));
+  }
+  // E_{nb-2} (written by the last k_stream) minus the changes of the last two blocks
+  const double *elast = ebuf[s->nb & 1];
+  const int sa = s->nb >= 2 ? (s->nb - 2) % 3 : -1, sb = (s->nb - 1) % 3;
   if (sharded) {
     if (!s->ex_eps || !s->ex_stats) { set_error("exchange buffers not set"); return -1; }
     Dev dx = d;
     dx.deps = s->ex_eps;
-    HIPCHK(launch_rows(dx, H_ROW_PENDING | H_ROW_WRITE | H_ROW_DEPS, nullptr, s->st));
+    HIPCHK(launch_rows(dx, H_ROW_PENDING | H_ROW_WRITE | H_ROW_DEPS, nullptr, s->st, elast, sa, sb));
   } else {
-    if (int rc = rows_flagged(s, H_ROW_PENDING | H_ROW_WRITE | H_ROW_REDUCE)) return rc;
+    HIPCHK(launch_rows(d, H_ROW_PENDING | H_ROW_WRITE | H_ROW_REDUCE, nullptr, s->st, elast, sa, sb));
   }
   const int mode = s->model == MODEL_HORSESHOE ? H_MR_HS : H_MR_BAYESR;
   HIPCHK(launch_markers(d, mode, it, s->st));
@@ -360,7 +432,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   s->log.fn = opt.log;
   s->log.user = opt.log_userdata;
   s->device = opt.device;
-  if (hipSetDevice(s->device) != hipSuccess || hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(s->device) != hipSuccess) {
     set_error("cannot initialise HIP device %d", s->device);
     delete s;
     return nullptr;
@@ -368,6 +440,41 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, s->device);
   const int cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  // Two queues for the lag-1 pipeline: k_solve(s) on one reserved CU overlaps k_stream(s+1)
+  // on the others.  The reservation guarantees the solver a CU while streaming workgroups wait
+  // on its device counters.  Without CU masks both kernels share one queue (same results).
+  {
+    const char *single = getenv("BRR_SINGLE_QUEUE");
+    bool ok = false;
+    if (!(single && single[0] == '1') && cus >= 2) {
+      std::vector<uint32_t> ma((size_t)(cus + 31) / 32, 0), mb((size_t)(cus + 31) / 32, 0);
+      for (int c = 0; c < cus; ++c) {
+        if (c == 0) mb[0] |= 1u;
+        else ma[(size_t)c / 32] |= 1u << (c % 32);
+      }
+      ok = hipExtStreamCreateWithCUMask(&s->st, (uint32_t)ma.size(), ma.data()) == hipSuccess &&
+           hipExtStreamCreateWithCUMask(&s->st2, (uint32_t)mb.size(), mb.data()) == hipSuccess;
+      if (!ok) {
+        if (s->st) (void)hipStreamDestroy(s->st);
+        if (s->st2) (void)hipStreamDestroy(s->st2);
+        s->st = s->st2 = nullptr;
+      }
+    }
+    if (!ok) {
+      if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) {
+        set_error("cannot create a stream on HIP device %d", s->device);
+        delete s;
+        return nullptr;
+      }
+      s->st2 = s->st;
+    }
+    if (hipEventCreateWithFlags(&s->ev_a, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_b, hipEventDisableTiming) != hipSuccess) {
+      set_error("cannot create events on HIP device %d", s->device);
+      delete s;
+      return nullptr;
+    }
+  }
   s->N = N; s->M = M; s->M_total = M_total; s->col_offset = col_offset;
   s->K = K; s->G = groups; s->F = (int)F; s->B = B; s->model = model;
   s->order_mode = opt.order_mode;
@@ -377,12 +484,13 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   Dev &d = s->d;
   d.N = N; d.ld = (N + 63) / 64 * 64; d.M = M; d.M_total = M_total; d.col_offset = col_offset;
   d.K = K; d.G = groups; d.F = (int)F; d.B = B; d.nb = s->nb; d.model = model;
-  // streaming geometry: ~2 workgroups per CU, 4 consecutive rows per lane (R multiple of 4)
-  const int64_t target = 2LL * cus;
-  d.R = (int)std::min<int64_t>(256, std::max<int64_t>(4, ((N + target - 1) / target + 3) / 4 * 4));
-  d.RG = (int)((N + d.R - 1) / d.R);
+  // streaming geometry: row tiles of SROWS rows (k_stream), NC = B/128 column chunks
+  d.R = SROWS;
+  d.RG = (int)((N + SROWS - 1) / SROWS);
   d.NG = (d.RG + STREAM_GROUP - 1) / STREAM_GROUP;
   const int NGpad = (d.NG + 31) / 32 * 32;  // k_solve reads slab2 in unconditional batches of 32
+  const int NC = B >= 128 ? B / 128 : 1;
+  (void)cus;
   d.MRG = (int)((M + 255) / 256);
   const int64_t RGrows = (N + 255) / 256;
   int rc = 0;
@@ -391,6 +499,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   rc |= s->alloc(const_cast<double **>(&d.fixed), N * std::max<int64_t>(F, 1));
   rc |= s->alloc(const_cast<double **>(&d.cva), (int64_t)groups * std::max(K - 1, 1));
   rc |= s->alloc(&d.eps, d.ld);  // padded to ld rows (zeros): k_stream loads 4 rows per lane
+  rc |= s->alloc(&d.eps2, d.ld);  // k_stream double buffer
   rc |= s->alloc(&d.eps_start, d.ld);
   rc |= s->alloc(&d.beta, M);
   rc |= s->alloc(&d.xsq, M);
@@ -403,17 +512,27 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   rc |= s->alloc(&d.forder, std::max<int64_t>(F, 1));
   rc |= s->alloc(&d.sel, M);
   rc |= s->alloc(&d.gram, (int64_t)s->nb * B * B);
+  rc |= s->alloc(&d.xgram, (int64_t)s->nb * B * B);
+  rc |= s->alloc(&d.xgramT, (int64_t)s->nb * B * B);
   rc |= s->alloc(&d.member, (int64_t)s->nb * B);
   rc |= s->alloc(&d.gidx, (int64_t)s->nb * B);
   rc |= s->alloc(&d.bsz, s->nb);
   rc |= s->alloc(&d.gblk, s->nb);
   rc |= s->alloc(&d.blkorder, s->nb);
-  rc |= s->alloc(&d.slab1, (int64_t)d.RG * B);
-  rc |= s->alloc(&d.slab2, (int64_t)NGpad * B);
-  rc |= s->alloc(&d.cnt1, d.NG);
-  rc |= s->alloc(&d.pend_idx, B);
-  rc |= s->alloc(&d.pend_bo, B);
-  rc |= s->alloc(&d.pend_bn, B);
+  d.slab1_stride = (int64_t)d.RG * B;
+  d.slab2_stride = (int64_t)NGpad * B;
+  d.pend_stride = B + 16;
+  rc |= s->alloc(&d.slab1, 2 * d.slab1_stride);
+  rc |= s->alloc(&d.slab2, 2 * d.slab2_stride);
+  rc |= s->alloc(&d.cnt1, 2 * (int64_t)d.NG * NC);
+  rc |= s->alloc(&d.gdone, 2);
+  rc |= s->alloc(&d.pend_idx, 3 * d.pend_stride);
+  rc |= s->alloc(&d.pend_gi, 3 * d.pend_stride);
+  rc |= s->alloc(&d.pend_bo, 3 * d.pend_stride);
+  rc |= s->alloc(&d.pend_bn, 3 * d.pend_stride);
+  rc |= s->alloc(&d.pend_n, 3);
+  d.nbB = (int64_t)s->nb * B;
+  rc |= s->alloc(&d.mc, d.nbB * (3 + 2 * std::max(K, 1)));
   rc |= s->alloc(&d.rslab, 2 * RGrows);
   rc |= s->alloc(&d.rcnt, 1);
   rc |= s->alloc(&d.mslab, (int64_t)d.MRG * s->NS);
@@ -425,14 +544,18 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   d.gAssign = nullptr;
   // every buffer a kernel may read before writing is zeroed here (recycled device memory
   // holds the previous session's values): slab2 pad rows, member padding, pending list
-  bool ok = hipMemsetAsync(d.cnt1, 0, sizeof(int) * d.NG, s->st) == hipSuccess &&
+  bool ok = hipMemsetAsync(d.cnt1, 0, sizeof(int) * 2 * d.NG * NC, s->st) == hipSuccess &&
+            hipMemsetAsync(d.gdone, 0, sizeof(int) * 2, s->st) == hipSuccess &&
+            hipMemsetAsync(d.pend_gi, 0, sizeof(int) * 3 * d.pend_stride, s->st) == hipSuccess &&
+            hipMemsetAsync(d.pend_n, 0, sizeof(int) * 3, s->st) == hipSuccess &&
             hipMemsetAsync(d.eps, 0, sizeof(double) * d.ld, s->st) == hipSuccess &&
-            hipMemsetAsync(d.slab2, 0, sizeof(double) * NGpad * B, s->st) == hipSuccess &&
+            hipMemsetAsync(d.eps2, 0, sizeof(double) * d.ld, s->st) == hipSuccess &&
+            hipMemsetAsync(d.slab2, 0, sizeof(double) * 2 * d.slab2_stride, s->st) == hipSuccess &&
             hipMemsetAsync(d.member, 0, sizeof(int) * s->nb * B, s->st) == hipSuccess &&
             hipMemsetAsync(d.gidx, 0, sizeof(int) * s->nb * B, s->st) == hipSuccess &&
-            hipMemsetAsync(d.pend_idx, 0, sizeof(int) * B, s->st) == hipSuccess &&
-            hipMemsetAsync(d.pend_bo, 0, sizeof(double) * B, s->st) == hipSuccess &&
-            hipMemsetAsync(d.pend_bn, 0, sizeof(double) * B, s->st) == hipSuccess &&
+            hipMemsetAsync(d.pend_idx, 0, sizeof(int) * 3 * d.pend_stride, s->st) == hipSuccess &&
+            hipMemsetAsync(d.pend_bo, 0, sizeof(double) * 3 * d.pend_stride, s->st) == hipSuccess &&
+            hipMemsetAsync(d.pend_bn, 0, sizeof(double) * 3 * d.pend_stride, s->st) == hipSuccess &&
             hipMemsetAsync(d.rcnt, 0, sizeof(int), s->st) == hipSuccess &&
             hipMemsetAsync(d.mcnt, 0, sizeof(int), s->st) == hipSuccess &&
             hipMemsetAsync(d.sc, 0, sizeof(Scal), s->st) == hipSuccess &&
@@ -629,7 +752,8 @@ int brr_session_init(brr_session *s, int32_t seed) {
   d.seed = (uint64_t)(int64_t)seed;
   // identity block layout -> Gram blocks and xsquared (BayesRv2.cpp:170)
   HIPCHK(launch_perm(d, 0, s->shard, true, s->st));
-  HIPCHK(launch_gram(d, s->nb, s->st));
+  HIPCHK(launch_gram(d, 0, d.gram, nullptr, s->st));
+  HIPCHK(launch_gram(d, 1, d.xgram, d.xgramT, s->st));  // cycle neighbours (b, b+1 mod nb)
   HIPCHK(launch_xsq(d, s->st));
   Scal sc{};
   if (s->model == MODEL_RESTART) { sc.mu = s->mu0; sc.sigmaE = s->sigmaE0; }
@@ -683,7 +807,7 @@ int brr_session_sweep(brr_session *s, int32_t n) {
     }
     if (int rc = do_sweep_finish(s)) return rc;
   }
-  return 0;
+  return check_device_error(s);
 }
 
 int brr_comm_unique_id(void *out) {
@@ -785,6 +909,11 @@ int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
     case BRR_SUMSQ_BETA: return d2h(s, out, s->d.stats, 1);
     case 100: *out = (double)sc.n_slow; return 0;     // diagnostics (not in brr.h)
     case 101: *out = (double)sc.n_changed; return 0;
+    case 102: *out = (double)sc.prof_on; return 0;
+    case 103: *out = s->st2 != s->st ? 2.0 : 1.0; return 0;  // queues used by the sweep pipeline
+    case 110: case 111: case 112: case 113: case 114: case 115: case 116: case 117: case 118: case 119:
+    case 120: case 121:
+      *out = (double)sc.prof[which - 110]; return 0;
     default: set_error("unknown scalar %d", which); return -1;
   }
 }
@@ -802,6 +931,10 @@ int brr_session_set_scalar(brr_session *s, int32_t which, double v) {
     case BRR_ETA: sc.eta = v; break;
     case BRR_C2: sc.c2 = v; break;
     case BRR_SIGMAG: return h2d(s, s->d.sigmaGG, &v, 1);
+    case 102:  // diagnostics: k_solve phase timers on/off (resets the totals)
+      sc.prof_on = v != 0.0;
+      for (auto &x : sc.prof) x = 0;
+      break;
     default: set_error("scalar %d not settable", which); return -1;
   }
   s->need_reduce = true;
@@ -880,7 +1013,10 @@ int brr_session_set_timing(brr_session *s, int32_t on) {
   if (!s) return -1;
   if (int rc = collect_timing(s)) return rc;
   s->timing = on != 0;
-  if (on) { s->t_stream = s->t_solve = 0; s->n_stream = s->n_solve = 0; }
+  if (on) {
+    s->t_stream = s->t_solve = s->t_solve_sweep = 0;
+    s->n_stream = s->n_solve = s->n_solve_sweep = 0;
+  }
   return 0;
 }
 
@@ -890,8 +1026,9 @@ int brr_session_timing(brr_session *s, double *stream_ms, int64_t *n_stream, dou
   if (int rc = collect_timing(s)) return rc;
   if (stream_ms) *stream_ms = s->t_stream;
   if (n_stream) *n_stream = s->n_stream;
-  if (solve_ms) *solve_ms = s->t_solve;
-  if (n_solve) *n_solve = s->n_solve;
+  // the persistent solver is timed per sweep: reported per block position (waits included)
+  if (solve_ms) *solve_ms = s->t_solve + s->t_solve_sweep;
+  if (n_solve) *n_solve = s->n_solve + s->n_solve_sweep * s->nb;
   return 0;
 }
 

@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--block-size", type=int, default=128)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--data-seed", type=int, default=20261015)
+    ap.add_argument("--profile-solve", action="store_true", help="k_solve phase timers (diag)")
+    ap.add_argument("--trace-sweeps", type=int, default=0, help="time N more sweeps one by one (diag)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-markers", type=int, default=3000,
                     help="markers in the bounded CPU-baseline sample (N as in the config)")
@@ -189,7 +191,18 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    s.sweep(args.warmup)
+    warm_trace = []
+    if args.trace_sweeps:
+        c0 = s.scalar(101)
+        for _ in range(args.warmup):
+            t1 = time.perf_counter()
+            s.sweep(1)
+            s.synchronize()
+            c1 = s.scalar(101)
+            warm_trace.append((round((time.perf_counter() - t1) * 1e3, 2), int(c1 - c0)))
+            c0 = c1
+    else:
+        s.sweep(args.warmup)
     barrier()
     t0 = time.perf_counter()
     s.sweep(args.steps)
@@ -223,6 +236,33 @@ def main():
                 "bytes_per_launch": int(bytes_launch),
                 "solve_avg_us": round(tm["solve_ms"] / max(1, tm["solve_launches"]) * 1e3, 3),
                 "sweep_hbm_gbs": round(4.0 * N * Pl / (ms * 1e-3) / 1e9, 1)}
+    if args.trace_sweeps:
+        # per-sweep wall time and changed markers of a fresh chain's first sweeps (diagnostic)
+        tr = []
+        s2 = s
+        c0 = s2.scalar(101)
+        for _ in range(args.trace_sweeps):
+            t1 = time.perf_counter()
+            s2.sweep(1)
+            s2.synchronize()
+            c1 = s2.scalar(101)
+            tr.append((round((time.perf_counter() - t1) * 1e3, 2), int(c1 - c0)))
+            c0 = c1
+        diag["sweep_trace_ms_changed"] = {"warmup": warm_trace, "after": tr}
+    if args.profile_solve:
+        # k_solve phase breakdown (device wall clock, 100 MHz) over two more sweeps
+        s.set_scalar(102, 1.0)
+        s.sweep(2)
+        calls = max(1.0, s.scalar(115))
+        diag["solve_phase_us"] = {k: round(s.scalar(110 + i) / calls / 100.0, 3) for i, k in
+                                  enumerate(["load", "gram_rows", "chain", "writeback"])}
+        diag["solve_chain_steps"] = round(s.scalar(116) / calls, 2)
+        diag["solve_refreshes"] = round(s.scalar(117) / calls, 2)
+        diag["solve_global_rows"] = round(s.scalar(114) / calls, 2)
+        diag["solve_refresh_us"] = round(s.scalar(118) / calls / 100.0, 3)
+        diag["solve_correct_us"] = round(s.scalar(119) / calls / 100.0, 3)
+        diag["solve_wait_us"] = round(s.scalar(120) / calls / 100.0, 3)
+        s.set_scalar(102, 0.0)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, P)
@@ -233,7 +273,7 @@ def main():
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (on-device Binomial(2,f) genotypes, standardised; f32 X, f64 arithmetic)",
             "config": {"workload": cfg["workload"], "N": N, "P": P, "K": K, "groups": G,
-                       "block_size": Bsz, "order": "blocked", "parallelism": f"column-shard x{world}",
+                       "block_size": Bsz, "order": "blocked", "queues": int(s.scalar(103)), "parallelism": f"column-shard x{world}",
                        "setup_s": round(t_setup, 2), "diag": diag},
             "roofline": roof, "cpu_baseline": cpu,
         }

@@ -174,7 +174,7 @@ static void random_shuffle_ref(glibc_rand *g, int32_t *a, int64_t n) {
   }
 }
 
-/* Philox Fisher-Yates (device fast-path spec, DESIGN.md "visit order") */
+/* Philox Fisher-Yates (device fast-path spec for the order inside a block, DESIGN.md "visit order") */
 static void fisher_yates(uint64_t seed, int32_t *a, int64_t n, uint32_t tag, uint32_t entity,
                          uint32_t it) {
   for (int64_t i = n - 1; i >= 1; --i) {
@@ -191,8 +191,15 @@ void orc_blocked_order(uint64_t seed, uint32_t it, int64_t P, int32_t B, int32_t
   int64_t nb = (P + B - 1) / B;
   int32_t *blk = (int32_t *)malloc(sizeof(int32_t) * (size_t)(nb > 0 ? nb : 1));
   int32_t *w = (int32_t *)malloc(sizeof(int32_t) * (size_t)B);
-  for (int64_t b = 0; b < nb; ++b) blk[b] = (int32_t)b;
-  fisher_yates(seed, blk, nb, ORC_T_PERM_BLOCK, (uint32_t)shard, it);
+  /* block cycle with a random rotation and direction: consecutive blocks in the visit order
+     are neighbours in the cycle, so the device path can precompute their cross-Gram blocks */
+  {
+    uint32_t w4[4];
+    philox_draw(seed, 0, ORC_T_PERM_BLOCK, (uint32_t)shard, it, w4);
+    int64_t rot = (int64_t)(((uint64_t)w4[0] * (uint64_t)nb) >> 32);
+    int64_t dir = (w4[1] & 1u) ? 1 : -1;
+    for (int64_t s2 = 0; s2 < nb; ++s2) blk[s2] = (int32_t)(((rot + dir * s2) % nb + nb) % nb);
+  }
   int64_t pos = 0;
   for (int64_t s = 0; s < nb; ++s) {
     int64_t b = blk[s];

@@ -111,6 +111,49 @@ def test_v2_block64_and_many_sweeps(brr, oracle_mod, require_gpu):
     _compare(s, orc, O, L, L.MODEL_V2, tag="B=64 20 sweeps")
 
 
+@pytest.mark.parametrize("B", [256, 512])
+def test_v2_large_blocks(brr, oracle_mod, require_gpu, B):
+    """Multi-chunk streaming grid, a partial last block, Gram-row slot overflow (sweep 1 changes
+    most markers: more candidates than LDS slots) and ragged N (not a multiple of 256 rows)."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    X, Y, _ = _cohort(O, 301, 1300, n_causal=40)
+    s, orc = _make(brr, O, L.MODEL_V2, X, Y, 0, B=B)
+    for it in range(5):
+        s.sweep(1)
+        orc.sweep(1)
+        _compare(s, orc, O, L, L.MODEL_V2, tag=f"B={B} it={it}")
+
+
+def test_single_queue_pipeline(brr, oracle_mod, require_gpu, monkeypatch):
+    """Without CU-masked queues the stream / solve kernels share one queue in dependency order
+    (same device protocol, nothing waits): identical results to the oracle."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    monkeypatch.setenv("BRR_SINGLE_QUEUE", "1")
+    X, Y, _ = _cohort(O, 290, 700, n_causal=30)
+    s, orc = _make(brr, O, L.MODEL_V2, X, Y, 0, B=128)
+    assert s.scalar(103) == 1.0
+    for it in range(4):
+        s.sweep(1)
+        orc.sweep(1)
+        _compare(s, orc, O, L, L.MODEL_V2, tag=f"single queue it={it}")
+
+
+def test_horseshoe_block512(brr, oracle_mod, require_gpu):
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P = 260, 700
+    X, Y, _ = _cohort(O, N, P, n_causal=30)
+    A = (1 / np.sqrt(N)) * 150 / (P - 150)
+    hs = dict(A=A, v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0)
+    s, orc = _make(brr, O, L.MODEL_HORSESHOE, X, Y, 0, B=512, hs=hs)
+    for it in range(4):
+        s.sweep(1)
+        orc.sweep(1)
+        _compare(s, orc, O, L, L.MODEL_HORSESHOE, tag=f"hs B=512 it={it}")
+
+
 def test_groups_fixed_effects(brr, oracle_mod, require_gpu):
     from bayesrrcpp_amd import _lib as L
     O = oracle_mod

@@ -100,6 +100,23 @@ def test_blocked_order_is_block_restricted_permutation(oracle_mod):
             size = min(B, P - blk * B)
             assert set((o[pos:pos + size] // B).tolist()) == {blk}
             pos += size
+    # block sequence: a rotation of the block cycle, forwards or backwards (consecutive blocks
+    # are cycle neighbours, so their cross-Gram blocks can be precomputed)
+    nb = (P + B - 1) // B
+    dirs = set()
+    for it in range(16):
+        o = oracle_mod.blocked_order(7, it, P, B)
+        starts = np.concatenate([[0], np.cumsum([min(B, P - b * B) for b in range(nb)])])
+        seq, pos = [], 0
+        while pos < P:
+            blk = int(o[pos] // B)
+            seq.append(blk)
+            pos += min(B, P - blk * B)
+        d = (seq[1] - seq[0]) % nb
+        assert d in (1, nb - 1)
+        dirs.add(d)
+        assert all((seq[i + 1] - seq[i]) % nb == d for i in range(nb - 1))
+    assert dirs == {1, nb - 1}
     assert not np.array_equal(oracle_mod.blocked_order(7, 0, P, B), oracle_mod.blocked_order(7, 1, P, B))
 
 
