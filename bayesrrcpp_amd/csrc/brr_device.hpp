@@ -34,8 +34,7 @@ struct Scal {
   double mu, mu_prev, sigmaE, sigmaF, tau, eta, c2;
   double S1;   // sum(eps + mu)   (BayesRv2.cpp:177-178 operand), from the latest row pass
   double S2;   // ||eps||^2        (BayesRv2.cpp:251 operand)
-  int pend_seq;  // blocks of the current sweep whose k_solve has published its changes
-  int err;       // device-side protocol error (a bounded wait timed out)
+  int pad0, pad1;
   unsigned long long n_slow;     // diagnostics: serial steps that needed the exact re-evaluation
   unsigned long long n_changed;  // diagnostics: markers whose beta changed
   int prof_on;                   // diagnostics: k_solve phase timers on
@@ -48,6 +47,19 @@ struct Hyper {
   double A, vL, vT, c2_0, vC, sC;         // Horseshoe
 };
 
+// Hand-over words of the stream / solve pipeline (MI355X_MICROARCH.md "Valid forms"): a block
+// of their own, each word on its own 128-B line, zeroed by hipMemsetAsync when the session is
+// created and afterwards only touched by agent-scope atomics / sc1 accesses.  Counts are
+// cumulative over the session (epochs), so nothing is ever reset inside a kernel.
+enum SyncWord : int {
+  SY_PEND = 0,     // blocks whose k_solve has published its change list (session total)
+  SY_GDONE = 32,   // + 32 * parity: level-2 reduction groups completed (session total)
+  SY_ERR = 96,     // a bounded wait expired; SY_ERR + 1..4: site, target, value seen, workgroup
+  SY_ARRIVE = 128, // persistent streamer workgroups that started (session total)
+  SY_TS = 160,     // diagnostics: 64-bit wall-clock stamps (see brr_session.cpp)
+  SY_WORDS = 192
+};
+
 // Stats vector (reduced over markers, summed across shards):
 //   [0] sum beta^2  [1] sum beta^2/lambda  [2 .. 2+G) betaAcum[g]  [2+G .. 2+G+G*K) v[g][k]
 __host__ __device__ inline int stats_size(int G, int K) { return 2 + G + G * K; }
@@ -56,6 +68,7 @@ __host__ __device__ inline int stats_size(int G, int K) { return 2 + G + G * K; 
 struct Dev {
   int64_t N, ld, M, M_total, col_offset;
   int K, G, F, B, nb, model, R, RG, NG, MRG;
+  int gtarget;      // reduction groups k_solve(s) waits for (per-block: NG * NC; persistent: NG)
   uint64_t seed;
   Hyper hyp;
   const float *X;
@@ -69,8 +82,11 @@ struct Dev {
   double *gram, *xgram, *xgramT;
   int *member, *gidx, *bsz, *gblk, *blkorder;
   double *slab1, *slab2;   // [2][RG*B], [2][NGpad*B]
-  int *cnt1;                // [2][NG*NC] level-2 arrival counters (k_stream)
-  int *gdone;               // [2] level-2 groups completed (k_stream -> k_solve)
+  int *cnt1;                // [2][NG*NC] level-2 arrival counters (k_stream), cumulative
+  int *sync;                // SyncWord block
+  int sbase;                // blocks published before this sweep (SY_PEND epoch base)
+  int gbase[2];             // blocks of each parity before this sweep (SY_GDONE / cnt1 epochs)
+  int abase;                // persistent streamer arrivals before this sweep (SY_ARRIVE epoch)
   int64_t slab1_stride, slab2_stride, pend_stride;
   int *pend_idx, *pend_gi;  // [3][B+16]
   double *pend_bo, *pend_bn;

@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "brr_device.hpp"
 #include "brr_rng.hpp"
 
@@ -100,10 +102,27 @@ __device__ __forceinline__ int ld_sc1_int(const int *p) {
 // the other queue.  Never spins forever: after ~0.5 s the protocol error flag is raised and the
 // caller proceeds (the host reports the error after the sweep).
 constexpr uint32_t SPIN_MAX = 1u << 22;
-__device__ __forceinline__ void wait_geq(const int *cnt, int target, int *err) {
-  for (uint32_t n = 0; ld_sc1_int(cnt) < target; ++n) {
-    if (n > SPIN_MAX) { atomicOr(err, 1); return; }
-    if ((n & 255) == 255 && ld_sc1_int(err)) return;  // an earlier wait already failed
+__device__ __forceinline__ void stamp(int *sync, int k) {  // first writer wins
+  unsigned long long *ts = reinterpret_cast<unsigned long long *>(sync + SY_TS) + k;
+  atomicCAS(ts, 0ull, (unsigned long long)wall_clock64());
+}
+
+__device__ __forceinline__ void wait_geq(const int *cnt, int target, int *sync, int where) {
+  for (uint32_t n = 0;; ++n) {
+    const int v = ld_sc1_int(cnt);
+    if (v >= target) return;
+    if (n == 0 && where == 2) stamp(sync, 6);
+    if (n > SPIN_MAX) {
+      stamp(sync, 7);
+      if (atomicCAS(sync + SY_ERR, 0, 1) == 0) {  // the first failure records where it happened
+        st_sc1_int(sync + SY_ERR + 1, where);
+        st_sc1_int(sync + SY_ERR + 2, target);
+        st_sc1_int(sync + SY_ERR + 3, v);
+        st_sc1_int(sync + SY_ERR + 4, (int)blockIdx.x);
+      }
+      return;
+    }
+    if ((n & 255) == 255 && ld_sc1_int(sync + SY_ERR)) return;  // an earlier wait already failed
     __builtin_amdgcn_s_sleep(8);
   }
 }
@@ -346,9 +365,6 @@ __global__ void k_sweep_start(Dev d, uint32_t it) {
   sc->mu_prev = sc->mu;
   const double z = normal(d.seed, T_MU, 0, it, 0);
   sc->mu = sc->S1 / (double)d.N + sqrt(sc->sigmaE / (double)d.N) * z;
-  sc->pend_seq = 0;
-  d.gdone[0] = 0;
-  d.gdone[1] = 0;
   if (d.model == MODEL_HORSESHOE) {
     const Hyper &h = d.hyp;
     sc->eta = inv_gamma_rate_rng(d.seed, 0.5 + 0.5 * h.vT,
@@ -770,7 +786,7 @@ __global__ __launch_bounds__(256, 2) void k_stream(Dev d, int s, const double *e
     // one wave stages the list in LDS (one sc1 request per line per workgroup, instead of one
     // per wave and entry hammering the same few lines from every workgroup)
     if (w == 0) {
-      if (lane == 0) wait_geq(&d.sc->pend_seq, s - 1, &d.sc->err);
+      if (lane == 0) wait_geq(d.sync + SY_PEND, d.sbase + s - 1, d.sync, 1);
       const int slot = (s - 2) % 3;
       const int np = ld_sc1_int(d.pend_n + slot);
       const int *pidx = d.pend_idx + slot * d.pend_stride;
@@ -824,7 +840,8 @@ __global__ __launch_bounds__(256, 2) void k_stream(Dev d, int s, const double *e
   const int grp = rg / STREAM_GROUP;
   const int g0 = grp * STREAM_GROUP;
   const int gsz = min(STREAM_GROUP, d.RG - g0);
-  if (last_arriver_wt(cnt1 + grp * NC + cc, gsz, &s_last)) {
+  const int use = d.gbase[par] + (s >> 1);  // earlier blocks of this parity (cumulative counters)
+  if (last_arriver_wt(cnt1 + grp * NC + cc, (use + 1) * gsz, &s_last)) {
     if (t < CB) {
       double v16[STREAM_GROUP];
 #pragma unroll
@@ -835,9 +852,45 @@ __global__ __launch_bounds__(256, 2) void k_stream(Dev d, int s, const double *e
       for (int q = 0; q < STREAM_GROUP; ++q) acc += v16[q];
       st_sc1(slab2 + (int64_t)grp * B + cc * CB + t, acc);
     }
-    if (t == 0) cnt1[grp * NC + cc] = 0;
-    publish_add(d.gdone + par, 1);  // k_solve(s) waits for NG * NC groups
+    publish_add(d.sync + SY_GDONE + 32 * par, 1);  // k_solve(s) waits for NG * NC groups
   }
+}
+
+// 16-column wave transpose-reduction (persistent streamer).
+__device__ __forceinline__ double wave_reduce16(double (&v)[16], int lane) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bool hi = lane & 32;
+    const double send = hi ? v[j] : v[j + 8];
+    const double keep = hi ? v[j + 8] : v[j];
+    v[j] = keep + __shfl_xor(send, 32);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool hi = lane & 16;
+    const double send = hi ? v[j] : v[j + 4];
+    const double keep = hi ? v[j + 4] : v[j];
+    v[j] = keep + __shfl_xor(send, 16);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const bool hi = lane & 8;
+    const double send = hi ? v[j] : v[j + 2];
+    const double keep = hi ? v[j + 2] : v[j];
+    v[j] = keep + __shfl_xor(send, 8);
+  }
+  {
+    const bool hi = lane & 4;
+    const double send = hi ? v[0] : v[1];
+    const double keep = hi ? v[1] : v[0];
+    v[0] = keep + __shfl_xor(send, 4);
+  }
+  const double a = v[0] + __shfl_xor(v[0], 2);
+  return a + __shfl_xor(a, 1);
+}
+// column held (lanes with (lane & 3) == 0) after wave_reduce16
+__device__ __forceinline__ int reduce16_col(int lane) {
+  return ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
 }
 
 // ------------------------------------------------------------------------------------
@@ -861,10 +914,11 @@ constexpr size_t SOLVE_LDS_MAX = 160 * 1024;
 // solver).  Phase A needs nothing from k_stream(s): per-position constants, the previous
 // block's changes and their cross-Gram correction.  Phase B waits for k_stream(s)'s reduction
 // groups, then decides, stages Gram rows, runs the serial chain and publishes.
-template <bool HS, int B>
+template <bool HS, int B, int NT>
 __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, int nslot, char *smem) {
 #pragma clang fp contract(off)
-  constexpr int NPT = (B + 255) / 256;  // positions per thread, parallel phases
+  constexpr int NPT = (B + NT - 1) / NT;  // positions per thread, parallel phases
+  constexpr int NW = NT / 64;             // waves
   constexpr int NS = B / 64;            // positions per lane (contiguous), serial chain
   const int K = HS ? 1 : d.K;
   const int KD = K > 1 ? K - 1 : 0;
@@ -885,7 +939,6 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   const double sigmaE = d.sc->sigmaE;
   const int64_t S = d.nbB;
   const int64_t q0 = (int64_t)s * B;
-  const int NC = B >= 128 ? B / 128 : 1;
 
   // A) everything that does not depend on k_stream(s)
   const double *C = nullptr;
@@ -903,7 +956,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   }
 #pragma unroll
   for (int c = 0; c < NPT; ++c) {
-    const int pos = t + 256 * c;
+    const int pos = t + NT * c;
     if (pos < bs) {
       const int64_t q = q0 + pos;
       const int gi = d.gidx[q];
@@ -941,12 +994,10 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       Lr0[pos] = corr;
     }
   }
-  // B) wait for k_stream(s)'s reduction groups (other queue), then re-arm the counter (the
-  //    next writer, k_stream(s+2), cannot start its reduction before this block publishes)
-  if (t == 0) {
-    wait_geq(d.gdone + par, d.NG * NC, &d.sc->err);
-    __hip_atomic_store(d.gdone + par, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  // B) wait for k_stream(s)'s reduction groups (other queue; cumulative count)
+  if (t == 0 && s == 0) stamp(d.sync, 3);
+  if (t == 0) wait_geq(d.sync + SY_GDONE + 32 * par, (d.gbase[par] + (s >> 1) + 1) * d.gtarget, d.sync, 3);
+  if (t == 0 && s == 0) stamp(d.sync, 4);
   __syncthreads();
   if (prof) tw = wall_clock64();
   const double *slab2 = d.slab2 + par * d.slab2_stride;
@@ -955,7 +1006,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   int base = 0;
 #pragma unroll
   for (int c = 0; c < NPT; ++c) {
-    const int pos = t + 256 * c;
+    const int pos = t + NT * c;
     bool likely = false;
     if (pos < bs) {
       double dsum = 0.0;
@@ -999,7 +1050,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       Lslot[pos] = sl;
       if (sl >= 0) Lspos[sl] = pos;
     }
-    base += misc[0] + misc[1] + misc[2] + misc[3];
+    for (int w = 0; w < NW; ++w) base += misc[w];
     __syncthreads();
   }
   const int nused = min(base, nslot);
@@ -1010,16 +1061,16 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     double2 *S2 = reinterpret_cast<double2 *>(slots);
     constexpr int H = B / 2;
     const int tot = nused * H;
-    for (int e0 = 0; e0 < tot; e0 += 256 * 8) {
+    for (int e0 = 0; e0 < tot; e0 += NT * 8) {
       double2 v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int e = min(e0 + u * 256 + t, tot - 1);
+        const int e = min(e0 + u * NT + t, tot - 1);
         v[u] = G2[(int64_t)Lgi[Lspos[e / H]] * H + (e % H)];
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        if (e0 + u * 256 + t < tot) S2[e0 + u * 256 + t] = v[u];
+        if (e0 + u * NT + t < tot) S2[e0 + u * NT + t] = v[u];
     }
   }
   __syncthreads();
@@ -1156,7 +1207,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   base = 0;
 #pragma unroll
   for (int c = 0; c < NPT; ++c) {
-    const int pos = t + 256 * c;
+    const int pos = t + NT * c;
     int changed = 0;
     double bnv = 0.0, bov = 0.0;
     int m = 0;
@@ -1184,7 +1235,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       st_sc1(pbo + idx, bov);
       st_sc1(pbn + idx, bnv);
     }
-    base += misc[0] + misc[1] + misc[2] + misc[3];
+    for (int w = 0; w < NW; ++w) base += misc[w];
     __syncthreads();
   }
   const int npend = base;
@@ -1200,7 +1251,8 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0) {
-    __hip_atomic_store(&d.sc->pend_seq, s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d.sync + SY_PEND, d.sbase + s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (s == 0) stamp(d.sync, 5);
     if (npend) atomicAdd(&d.sc->n_changed, (unsigned long long)npend);
     if (prof) {
       const uint64_t tp4 = wall_clock64();
@@ -1217,19 +1269,189 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
 template <bool HS, int B>
 __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it, int nslot) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  solve_block<HS, B>(d, s, it, nslot, smem);
+  solve_block<HS, B, 256>(d, s, it, nslot, smem);
 }
 
-// Persistent solver: one launch per sweep on the solve queue's reserved CU, looping over the
-// block positions; each iteration's phase A (prefetch) overlaps the wait for k_stream(s).
-template <bool HS, int B>
-__global__ __launch_bounds__(256) void k_solve_sweep(Dev d, uint32_t it, int nslot) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  for (int s = 0; s < d.nb; ++s) {
-    solve_block<HS, B>(d, s, it, nslot, smem);
-    __syncthreads();
+
+// ------------------------------------------------------------------------------------
+// k_sweep: the whole marker loop of a sweep in ONE persistent launch.  Workgroup 0 is the
+// solver (solve_block for s = 0..nb-1); workgroups 1..nsg stream.  Every workgroup has its own
+// CU (the solver's LDS needs it), all are resident (census at the start), so the device
+// counters of the lag-1 hand-over can be waited on (bounded).
+//
+// Streaming workgroup g = two halves of 256 threads; half h owns the row tiles
+// [vg RG / nvg, (vg+1) RG / nvg) of vg = 2g + h for the whole sweep and keeps their residual in
+// LDS.  Per block s it applies block s-2's changes (after the solver's counter says they are
+// published), forms the partial dots X_s^T E_{s-1} of its rows in (chunk, tile) items of CW
+// columns per wave -- both halves run the same item count, so the workgroup's barriers stay
+// uniform -- and reduces them across workgroups (groups of 8 workgroups = 16 row slices, last
+// arriver, write-through) for the solver.  The next item's X loads, across block boundaries,
+// are issued before the current item is consumed, so HBM stays busy while a workgroup waits.
+// At the end it applies the last two blocks' changes and writes eps back.
+constexpr int SWEEP_NT = 512;
+constexpr int FUSED_GROUP = 8;  // streaming workgroups per level-2 reduction group
+
+__device__ __forceinline__ void apply_pending_half(const Dev &d, int slot, int tile0, int nth, double *eps_h,
+                                                   int *s_pidx, double *s_pbo, double *s_pbn, int *s_np) {
+#pragma clang fp contract(off)
+  const int t = threadIdx.x, lane = t & 63;
+  const int wh = (t >> 6) & 3;
+  if (t < 64) {
+    const int np = ld_sc1_int(d.pend_n + slot);
+    const int *pidx = d.pend_idx + slot * d.pend_stride;
+    const double *pbo = d.pend_bo + slot * d.pend_stride, *pbn = d.pend_bn + slot * d.pend_stride;
+    for (int e = lane; e < np; e += 64) {
+      s_pidx[e] = ld_sc1_int(pidx + e);
+      s_pbo[e] = ld_sc1(pbo + e);
+      s_pbn[e] = ld_sc1(pbn + e);
+    }
+    if (lane == 0) *s_np = np;
+  }
+  __syncthreads();
+  const int np = *s_np;
+  for (int k = wh; k < nth; k += 4) {
+    const int64_t row0 = (int64_t)(tile0 + k) * SROWS + 4 * lane;
+    const bool valid = row0 < d.N;
+    const float *Xr = d.X + (valid ? row0 : 0);
+    double *e = eps_h + k * SROWS + 4 * lane;
+    double e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
+    for (int p0 = 0; p0 < np; p0 += 8) {
+      float4 xp[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) xp[q] = *reinterpret_cast<const float4 *>(Xr + (int64_t)s_pidx[p0 + q] * d.ld);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const double bo = s_pbo[p0 + q], bn = s_pbn[p0 + q];
+        const double a0 = xp[q].x, a1 = xp[q].y, a2 = xp[q].z, a3 = xp[q].w;
+        e0 = (e0 + a0 * bo) - a0 * bn;  // BayesRv2.cpp:191,243
+        e1 = (e1 + a1 * bo) - a1 * bn;
+        e2 = (e2 + a2 * bo) - a2 * bn;
+        e3 = (e3 + a3 * bo) - a3 * bn;
+      }
+    }
+    if (valid) { e[0] = e0; e[1] = e1; e[2] = e2; e[3] = e3; }
+  }
+  __syncthreads();
+}
+
+template <int CW>
+__device__ __forceinline__ void stream_role(const Dev &d, int g, int nsg, int tmax, double *s_eps, int *s_pidx,
+                                            double *s_pbo, double *s_pbn, int *s_np, int *s_last) {
+#pragma clang fp contract(off)
+  const int t = threadIdx.x, lane = t & 63;
+  const int h = t >> 8;
+  const int wh = __builtin_amdgcn_readfirstlane((t >> 6) & 3);
+  const int nvg = 2 * nsg, vg = 2 * g + h;
+  const int tile0 = (int)((int64_t)vg * d.RG / nvg), tile1 = (int)((int64_t)(vg + 1) * d.RG / nvg);
+  const int nth = tile1 - tile0;  // <= tmax
+  const int B = d.B, nb = d.nb;
+  const int64_t ld = d.ld;
+  double *eps_h = s_eps + h * tmax * SROWS;
+  for (int i = t & 255; i < tmax * SROWS; i += 256) {
+    const int64_t row = (int64_t)tile0 * SROWS + i;
+    eps_h[i] = (i < nth * SROWS && row < d.N) ? d.eps[row] : 0.0;
+  }
+  __syncthreads();
+  const int CPW = B / 4;        // columns per wave
+  const int NCH = CPW / CW;     // chunks per wave and block
+  const int items = NCH * tmax; // (chunk, tile) items per wave and block, same in both halves
+  const int total = items * nb;
+  const int grp = g / FUSED_GROUP, gw0 = grp * FUSED_GROUP, gsz = min(FUSED_GROUP, nsg - gw0);
+  auto issue = [&](int it, float4 (&x)[CW]) {
+    const int s = it / items, rem = it - s * items;
+    const int c = rem / tmax, k = rem - c * tmax;
+    const int64_t row0 = (int64_t)(tile0 + k) * SROWS + 4 * lane;
+    const float *Xr = d.X + ((k < nth && row0 < d.N) ? row0 : 0);  // padding tiles: eps = 0
+    const int *mem = d.member + (int64_t)s * B + wh * CPW + c * CW;  // wave-uniform: scalar loads
+#pragma unroll
+    for (int j = 0; j < CW; ++j) x[j] = *reinterpret_cast<const float4 *>(Xr + (int64_t)mem[j] * ld);
+  };
+  float4 xa[CW], xb[CW];
+  double v[CW];
+#pragma unroll
+  for (int j = 0; j < CW; ++j) v[j] = 0.0;
+  if (total > 0) issue(0, xa);
+  for (int it = 0; it < total; ++it) {
+    const int s = it / items, rem = it - s * items;
+    const int c = rem / tmax, k = rem - c * tmax;
+    if (rem == 0 && s >= 2) {
+      // block boundary: bring the residual rows from E_{s-2} to E_{s-1} (block s-2's changes)
+      if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + s - 1, d.sync, 2);
+      apply_pending_half(d, (s - 2) % 3, tile0, nth, eps_h, s_pidx, s_pbo, s_pbn, s_np);
+    }
+    // prefetch the next item (possibly the next block's first) before consuming this one
+    if (it + 1 < total) issue(it + 1, xb);
+    const double *e = eps_h + k * SROWS + 4 * lane;
+    const double e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
+#pragma unroll
+    for (int j = 0; j < CW; ++j)
+      v[j] += (((double)xa[j].x * e0 + (double)xa[j].y * e1) + (double)xa[j].z * e2) + (double)xa[j].w * e3;
+#pragma unroll
+    for (int j = 0; j < CW; ++j) xa[j] = xb[j];
+    if (k == tmax - 1) {
+      // chunk done over this half's tiles: wave-reduce its CW columns
+      const double r = wave_reduce16(v, lane);
+#pragma unroll
+      for (int j = 0; j < CW; ++j) v[j] = 0.0;
+      const int par = s & 1;
+      const int col = wh * CPW + c * CW + reduce16_col(lane);
+      if ((lane & 3) == 0) st_sc1(d.slab1 + par * d.slab1_stride + (int64_t)vg * B + col, r);
+      if (c == NCH - 1) {
+        // block done: level-2 reduction over the group's row slices, then publish
+        const double *slab1 = d.slab1 + par * d.slab1_stride;
+        int *cnt1 = d.cnt1 + par * d.NG;
+        const int use = d.gbase[par] + (s >> 1);
+        if (last_arriver_wt(cnt1 + grp, (use + 1) * gsz, s_last)) {
+          const int r0 = 2 * gw0, nr = 2 * gsz;
+          for (int cl = t; cl < B; cl += SWEEP_NT) {
+            double v16[2 * FUSED_GROUP];
+#pragma unroll
+            for (int q = 0; q < 2 * FUSED_GROUP; ++q)
+              v16[q] = q < nr ? ld_sc1(slab1 + (int64_t)(r0 + q) * B + cl) : 0.0;
+            double acc = 0.0;
+#pragma unroll
+            for (int q = 0; q < 2 * FUSED_GROUP; ++q) acc += v16[q];
+            st_sc1(d.slab2 + par * d.slab2_stride + (int64_t)grp * B + cl, acc);
+          }
+          publish_add(d.sync + SY_GDONE + 32 * par, 1);
+        }
+      }
+    }
+  }
+  // end of sweep: the last two blocks' changes, then the residual rows back to HBM
+  if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + nb, d.sync, 4);
+  if (nb >= 2) apply_pending_half(d, (nb - 2) % 3, tile0, nth, eps_h, s_pidx, s_pbo, s_pbn, s_np);
+  else __syncthreads();
+  apply_pending_half(d, (nb - 1) % 3, tile0, nth, eps_h, s_pidx, s_pbo, s_pbn, s_np);
+  for (int i = t & 255; i < nth * SROWS; i += 256) {
+    const int64_t row = (int64_t)tile0 * SROWS + i;
+    if (row < d.N) d.eps[row] = eps_h[i];
   }
 }
+
+template <bool HS, int B>
+__global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int nslot, int nsg, int tmax) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int s_last, s_np;
+  __shared__ int s_pidx[BMAX + 16];
+  __shared__ double s_pbo[BMAX + 16], s_pbn[BMAX + 16];
+  // residency census: every workgroup must be running before any waits on another
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(d.sync + SY_ARRIVE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    wait_geq(d.sync + SY_ARRIVE, d.abase + nsg + 1, d.sync, 5);
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    for (int s = 0; s < d.nb; ++s) {
+      solve_block<HS, B, SWEEP_NT>(d, s, it, nslot, smem);
+      __syncthreads();
+    }
+  } else {
+    stream_role<16>(d, (int)blockIdx.x - 1, nsg, tmax, reinterpret_cast<double *>(smem), s_pidx, s_pbo, s_pbn,
+                    &s_np, &s_last);
+  }
+}
+
 
 // ------------------------------------------------------------------------------------
 // Marker pass: Horseshoe v / lambda draws (HorseshoeR.cpp:218,242) and the statistics the
@@ -1454,6 +1676,16 @@ hipError_t launch_rows(const Dev &d, int flags, const double *deps_in, hipStream
   return hipGetLastError();
 }
 
+__global__ void k_noop() {}
+
+// A no-op dispatch right after an event record on the main queue: the event then completes
+// with this kernel, never with the persistent streamer that follows (which waits for the
+// solver queue that waits for the event).
+hipError_t launch_noop(hipStream_t st) {
+  hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, st);
+  return hipGetLastError();
+}
+
 hipError_t launch_sweep_start(const Dev &d, uint32_t it, hipStream_t st) {
   hipLaunchKernelGGL(k_sweep_start, dim3(1), dim3(64), 0, st, d, it);
   return hipGetLastError();
@@ -1477,6 +1709,66 @@ hipError_t launch_stream(const Dev &d, int s, const double *eps_in, double *eps_
     hipLaunchKernelGGL(k_stream<32>, dim3(grid), dim3(256), 0, st, d, s, eps_in, eps_out);
   else
     hipLaunchKernelGGL(k_stream<16>, dim3(grid), dim3(256), 0, st, d, s, eps_in, eps_out);
+  return hipGetLastError();
+}
+
+// Fused sweep geometry: one solver + nsg streaming workgroups, one per CU (the solver's LDS),
+// each half of a streaming workgroup owning at most tmax row tiles.  Returns false when the
+// configuration cannot be made resident (the per-block kernels are used then).
+template <bool HS, int B>
+static const void *sweep_fn() { return (const void *)k_sweep<HS, B>; }
+
+static const void *sweep_kernel(int model, int B) {
+  const bool hs = model == MODEL_HORSESHOE;
+  switch (B) {
+    case 64: return hs ? sweep_fn<true, 64>() : sweep_fn<false, 64>();
+    case 128: return hs ? sweep_fn<true, 128>() : sweep_fn<false, 128>();
+    case 256: return hs ? sweep_fn<true, 256>() : sweep_fn<false, 256>();
+    default: return hs ? sweep_fn<true, 512>() : sweep_fn<false, 512>();
+  }
+}
+
+bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
+  if (cus < 2 || d.B % 64 != 0) return false;
+  int nsg = std::min(cus - 1, (d.RG + 1) / 2);
+  if (max_wg > 0) nsg = std::min(nsg, max_wg);
+  nsg = std::max(nsg, 1);
+  const int tmax = (d.RG + 2 * nsg - 1) / (2 * nsg);
+  const void *fn = sweep_kernel(d.model, d.B);
+  hipFuncAttributes attr;
+  if (hipFuncGetAttributes(&attr, fn) != hipSuccess) return false;
+  const size_t budget = SOLVE_LDS_MAX - attr.sharedSizeBytes;
+  const int K = d.model == MODEL_HORSESHOE ? 1 : d.K;
+  const size_t fixed = solve_fixed_bytes(d.B, K);
+  if (fixed + 8 * (size_t)d.B > budget) return false;
+  const int nslot = (int)std::min<size_t>((size_t)d.B, (budget - fixed) / (8 * (size_t)d.B));
+  const size_t eps_bytes = (size_t)2 * tmax * SROWS * sizeof(double);
+  const size_t lds = std::max(fixed + (size_t)nslot * 8 * d.B, eps_bytes);
+  if (lds > budget) return false;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) != hipSuccess) return false;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, SWEEP_NT, lds) != hipSuccess || per_cu < 1)
+    return false;
+  cfg->nsg = nsg;
+  cfg->tmax = tmax;
+  cfg->nslot = nslot;
+  cfg->ngroups = (nsg + FUSED_GROUP - 1) / FUSED_GROUP;
+  cfg->lds = lds;
+  return true;
+}
+
+hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipStream_t st) {
+  const bool hs = d.model == MODEL_HORSESHOE;
+  const dim3 grid((unsigned)(c.nsg + 1)), blk(SWEEP_NT);
+#define BRR_SWEEP_LAUNCH(HSV, BV) \
+  hipLaunchKernelGGL((k_sweep<HSV, BV>), grid, blk, c.lds, st, d, it, c.nslot, c.nsg, c.tmax)
+  switch (d.B) {
+    case 64: if (hs) BRR_SWEEP_LAUNCH(true, 64); else BRR_SWEEP_LAUNCH(false, 64); break;
+    case 128: if (hs) BRR_SWEEP_LAUNCH(true, 128); else BRR_SWEEP_LAUNCH(false, 128); break;
+    case 256: if (hs) BRR_SWEEP_LAUNCH(true, 256); else BRR_SWEEP_LAUNCH(false, 256); break;
+    default: if (hs) BRR_SWEEP_LAUNCH(true, 512); else BRR_SWEEP_LAUNCH(false, 512); break;
+  }
+#undef BRR_SWEEP_LAUNCH
   return hipGetLastError();
 }
 
@@ -1511,25 +1803,6 @@ static void launch_solve_b(const Dev &d, int s, uint32_t it, hipStream_t st) {
   }
 }
 
-template <bool HS>
-static void launch_solve_sweep_b(const Dev &d, uint32_t it, hipStream_t st) {
-  const int K = HS ? 1 : d.K;
-  const int ns = solve_slots(d.B, K);
-  const size_t lds = solve_lds_bytes(d.B, K);
-  switch (d.B) {
-    case 64: hipLaunchKernelGGL((k_solve_sweep<HS, 64>), dim3(1), dim3(256), lds, st, d, it, ns); break;
-    case 128: hipLaunchKernelGGL((k_solve_sweep<HS, 128>), dim3(1), dim3(256), lds, st, d, it, ns); break;
-    case 256: hipLaunchKernelGGL((k_solve_sweep<HS, 256>), dim3(1), dim3(256), lds, st, d, it, ns); break;
-    default: hipLaunchKernelGGL((k_solve_sweep<HS, 512>), dim3(1), dim3(256), lds, st, d, it, ns); break;
-  }
-}
-
-hipError_t launch_solve_sweep(const Dev &d, uint32_t it, hipStream_t st) {
-  if (d.model == MODEL_HORSESHOE) launch_solve_sweep_b<true>(d, it, st);
-  else launch_solve_sweep_b<false>(d, it, st);
-  return hipGetLastError();
-}
-
 hipError_t launch_solve(const Dev &d, int s, uint32_t it, hipStream_t st) {
   if (d.model == MODEL_HORSESHOE) launch_solve_b<true>(d, s, it, st);
   else launch_solve_b<false>(d, s, it, st);
@@ -1541,14 +1814,10 @@ hipError_t set_solve_lds_limit(int /*B*/) {
   // session silently shrank the LDS window of later launches (out-of-range LDS writes are
   // dropped, no fault).
   const int lds = (int)SOLVE_LDS_MAX;
-  const void *fns[16] = {(const void *)k_solve<true, 64>, (const void *)k_solve<false, 64>,
-                         (const void *)k_solve<true, 128>, (const void *)k_solve<false, 128>,
-                         (const void *)k_solve<true, 256>, (const void *)k_solve<false, 256>,
-                         (const void *)k_solve<true, 512>, (const void *)k_solve<false, 512>,
-                         (const void *)k_solve_sweep<true, 64>, (const void *)k_solve_sweep<false, 64>,
-                         (const void *)k_solve_sweep<true, 128>, (const void *)k_solve_sweep<false, 128>,
-                         (const void *)k_solve_sweep<true, 256>, (const void *)k_solve_sweep<false, 256>,
-                         (const void *)k_solve_sweep<true, 512>, (const void *)k_solve_sweep<false, 512>};
+  const void *fns[8] = {(const void *)k_solve<true, 64>, (const void *)k_solve<false, 64>,
+                        (const void *)k_solve<true, 128>, (const void *)k_solve<false, 128>,
+                        (const void *)k_solve<true, 256>, (const void *)k_solve<false, 256>,
+                        (const void *)k_solve<true, 512>, (const void *)k_solve<false, 512>};
   for (const void *f : fns) {
     hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;

@@ -23,12 +23,18 @@ hipError_t launch_xsq(const Dev &d, hipStream_t st);
 hipError_t launch_rows(const Dev &d, int flags, const double *deps_in, hipStream_t st,
                        const double *eps_in = nullptr, int slot_a = -1, int slot_b = -1);
 hipError_t launch_sweep_start(const Dev &d, uint32_t it, hipStream_t st);
+hipError_t launch_noop(hipStream_t st);
 hipError_t launch_perm(const Dev &d, uint32_t it, int shard, bool identity, hipStream_t st);
 hipError_t launch_fixed(const Dev &d, uint32_t it, bool perm_on_device, hipStream_t st);
 hipError_t launch_stream(const Dev &d, int s, const double *eps_in, double *eps_out, hipStream_t st);
 hipError_t launch_prep(const Dev &d, uint32_t it, hipStream_t st);
+struct FusedCfg {
+  int nsg = 0, tmax = 0, nslot = 0, ngroups = 0;
+  size_t lds = 0;
+};
+bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg);
+hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipStream_t st);
 hipError_t launch_solve(const Dev &d, int s, uint32_t it, hipStream_t st);
-hipError_t launch_solve_sweep(const Dev &d, uint32_t it, hipStream_t st);
 hipError_t set_solve_lds_limit(int B);
 size_t solve_lds_bytes(int B, int K);
 hipError_t launch_markers(const Dev &d, int mode, uint32_t it, hipStream_t st);

@@ -120,9 +120,9 @@ struct brr_session {
   Logger log;
   Dev d{};
   int device = 0;
-  hipStream_t st = nullptr;   // main queue: streaming + everything else (all CUs but one)
-  hipStream_t st2 = nullptr;  // solve queue (one reserved CU); == st when CU masks are unavailable
-  hipEvent_t ev_a = nullptr, ev_b = nullptr;  // sweep-boundary joins of the two queues
+  hipStream_t st = nullptr;
+  int sbase = 0, gbase[2] = {0, 0}, abase = 0;  // hand-over counter epochs (see SyncWord)
+  FusedCfg fused;       // fused persistent sweep (nsg == 0: per-block kernels)
   int64_t N = 0, M = 0, M_total = 0, col_offset = 0;
   int K = 1, G = 1, F = 0, B = 128, nb = 0, model = 0, NS = 0;
   int order_mode = BRR_ORDER_BLOCKED;
@@ -156,11 +156,7 @@ struct brr_session {
     if (st) (void)hipStreamSynchronize(st);
     if (comm) (void)ncclCommDestroy(comm);
     for (void *p : allocs) (void)hipFree(p);
-    if (st2 && st2 != st) (void)hipStreamSynchronize(st2);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
-    if (ev_a) (void)hipEventDestroy(ev_a);
-    if (ev_b) (void)hipEventDestroy(ev_b);
-    if (st2 && st2 != st) (void)hipStreamDestroy(st2);
     if (st) (void)hipStreamDestroy(st);
   }
   hipEvent_t ev() {
@@ -188,7 +184,8 @@ int collect_timing(brr_session *s) {
     HIPCHK(hipEventElapsedTime(&ms, s->ev_pool[pr.first], s->ev_pool[pr.first + 1]));
     if (pr.second == 0) { s->t_stream += ms; s->n_stream++; }
     else if (pr.second == 1) { s->t_solve += ms; s->n_solve++; }
-    else { s->t_solve_sweep += ms; s->n_solve_sweep++; }
+    else if (pr.second == 2) { s->t_solve_sweep += ms; s->n_solve_sweep++; }
+    else { s->t_stream += ms; s->n_stream += s->nb; }  // persistent streamer: per block position
   }
   s->ev_pairs.clear();
   s->ev_used = 0;
@@ -217,11 +214,23 @@ int upload_order(brr_session *s, const std::vector<int32_t> &order) {
 
 // the pipeline's bounded device waits raise sc->err instead of hanging
 int check_device_error(brr_session *s) {
-  int err = 0;
   HIPCHK(hipStreamSynchronize(s->st));
-  HIPCHK(hipMemcpy(&err, &s->d.sc->err, sizeof err, hipMemcpyDeviceToHost));
-  if (err) {
-    set_error("device pipeline protocol timed out (k_stream / k_solve hand-over)");
+  std::vector<int> sy(SY_WORDS);
+  HIPCHK(hipMemcpy(sy.data(), s->d.sync, sizeof(int) * SY_WORDS, hipMemcpyDeviceToHost));
+  if (sy[SY_ERR]) {
+    set_error("device pipeline protocol timed out (k_stream / k_solve hand-over): site %d, workgroup %d "
+              "waited for %d, saw %d (iteration %d; published blocks %d, groups %d/%d)",
+              sy[SY_ERR + 1], sy[SY_ERR + 4], sy[SY_ERR + 2], sy[SY_ERR + 3], (int)s->iteration, sy[SY_PEND],
+              sy[SY_GDONE], sy[SY_GDONE + 32]);
+    const unsigned long long *ts = reinterpret_cast<const unsigned long long *>(sy.data() + SY_TS);
+    std::string msg = brr_last_error();
+    char buf[512];
+    std::snprintf(buf, sizeof buf, " [us from streamer start: census %.1f, solver entry %.1f, solver block-0 wait %.1f..%.1f, "
+                  "publish %.1f, first block-2 wait %.1f, first timeout %.1f]",
+                  (ts[1] - ts[0]) / 100.0, ((double)ts[2] - ts[0]) / 100.0, ((double)ts[3] - ts[0]) / 100.0,
+                  ((double)ts[4] - ts[0]) / 100.0, ((double)ts[5] - ts[0]) / 100.0, ((double)ts[6] - ts[0]) / 100.0,
+                  ((double)ts[7] - ts[0]) / 100.0);
+    set_error("%s%s", msg.c_str(), buf);
     return -3;
   }
   return 0;
@@ -260,62 +269,66 @@ int do_sweep_local(brr_session *s) {
     HIPCHK(launch_fixed(d, it, s->order_mode == BRR_ORDER_BLOCKED, s->st));
   if (sharded)
     if (int rc = rows_flagged(s, H_ROW_SNAPSHOT)) return rc;
+  // epoch bases of the hand-over counters (cumulative over the session)
+  d.sbase = s->sbase;
+  d.gbase[0] = s->gbase[0];
+  d.gbase[1] = s->gbase[1];
+  d.abase = s->abase;
+  if (s->fused.nsg > 0) s->abase += s->fused.nsg + 1;
+  s->sbase += s->nb;
+  s->gbase[0] += (s->nb + 1) / 2;
+  s->gbase[1] += s->nb / 2;
   // per-marker constants of the sweep in visit order
   HIPCHK(launch_prep(d, it, s->st));
-  // the hot loop (lag-1 pipeline): k_stream(b) on the main queue overlaps k_solve(b-1) on the
-  // solve queue; the kernels hand over through device counters (pend_seq, gdone).  eps
-  // alternates between the two buffers (k_stream reads one, writes the other).  Enqueue order
-  // stream(0), stream(1), solve(0), stream(2), solve(1), ... keeps every dependency ahead in
-  // queue order, so a single queue (no CU masks) runs the same protocol without waiting.
-  const bool two = s->st2 != s->st;
-  if (two) {
-    HIPCHK(hipEventRecord(s->ev_a, s->st));
-    HIPCHK(hipStreamWaitEvent(s->st2, s->ev_a, 0));
-  }
+  // the hot loop (lag-1 pipeline).  Fused: ONE persistent launch, workgroup 0 solves block s
+  // while the streaming workgroups form block s+1's dots (device counters hand over).
+  // Per-block fallback: stream(0), stream(1), solve(0), stream(2), solve(1), ... on the one
+  // queue (every dependency ahead in queue order, the same device protocol never waits).
   double *ebuf[2] = {d.eps, d.eps2};
-  auto stream_b = [&](int b) -> int {
-    const double *ein = ebuf[b & 1];
-    double *eout = ebuf[(b + 1) & 1];
+  const bool fused = s->fused.nsg > 0;
+  if (fused) {
+    Dev dp = d;
+    dp.NG = s->fused.ngroups;
+    dp.gtarget = s->fused.ngroups;
     if (s->timing) {
       const size_t i0 = s->ev_used;
       hipEvent_t e0 = s->ev(), e1 = s->ev();
       HIPCHK(hipEventRecord(e0, s->st));
-      HIPCHK(launch_stream(d, b, ein, eout, s->st));
+      HIPCHK(launch_sweep_fused(dp, it, s->fused, s->st));
       HIPCHK(hipEventRecord(e1, s->st));
-      s->ev_pairs.push_back({i0, 0});
+      s->ev_pairs.push_back({i0, 3});
     } else {
-      HIPCHK(launch_stream(d, b, ein, eout, s->st));
+      HIPCHK(launch_sweep_fused(dp, it, s->fused, s->st));
     }
-    return 0;
-  };
-  auto solve_b = [&](int b) -> int {
-    if (s->timing) {
-      const size_t i2 = s->ev_used;
-      hipEvent_t e2 = s->ev(), e3 = s->ev();
-      HIPCHK(hipEventRecord(e2, s->st2));
-      HIPCHK(launch_solve(d, b, it, s->st2));
-      HIPCHK(hipEventRecord(e3, s->st2));
-      s->ev_pairs.push_back({i2, 1});
-    } else {
-      HIPCHK(launch_solve(d, b, it, s->st2));
-    }
-    return 0;
-  };
-  if (two) {
-    // persistent solver on the reserved CU: one launch per sweep
-    if (s->timing) {
-      const size_t i2 = s->ev_used;
-      hipEvent_t e2 = s->ev(), e3 = s->ev();
-      HIPCHK(hipEventRecord(e2, s->st2));
-      HIPCHK(launch_solve_sweep(d, it, s->st2));
-      HIPCHK(hipEventRecord(e3, s->st2));
-      s->ev_pairs.push_back({i2, 2});
-    } else {
-      HIPCHK(launch_solve_sweep(d, it, s->st2));
-    }
-    for (int b = 0; b < s->nb; ++b)
-      if (int rc = stream_b(b)) return rc;
   } else {
+    auto stream_b = [&](int b) -> int {
+      const double *ein = ebuf[b & 1];
+      double *eout = ebuf[(b + 1) & 1];
+      if (s->timing) {
+        const size_t i0 = s->ev_used;
+        hipEvent_t e0 = s->ev(), e1 = s->ev();
+        HIPCHK(hipEventRecord(e0, s->st));
+        HIPCHK(launch_stream(d, b, ein, eout, s->st));
+        HIPCHK(hipEventRecord(e1, s->st));
+        s->ev_pairs.push_back({i0, 0});
+      } else {
+        HIPCHK(launch_stream(d, b, ein, eout, s->st));
+      }
+      return 0;
+    };
+    auto solve_b = [&](int b) -> int {
+      if (s->timing) {
+        const size_t i2 = s->ev_used;
+        hipEvent_t e2 = s->ev(), e3 = s->ev();
+        HIPCHK(hipEventRecord(e2, s->st));
+        HIPCHK(launch_solve(d, b, it, s->st));
+        HIPCHK(hipEventRecord(e3, s->st));
+        s->ev_pairs.push_back({i2, 1});
+      } else {
+        HIPCHK(launch_solve(d, b, it, s->st));
+      }
+      return 0;
+    };
     for (int b = 0; b < s->nb; ++b) {
       if (int rc = stream_b(b)) return rc;
       if (b >= 1)
@@ -323,13 +336,10 @@ int do_sweep_local(brr_session *s) {
     }
     if (int rc = solve_b(s->nb - 1)) return rc;
   }
-  if (two) {
-    HIPCHK(hipEventRecord(s->ev_b, s->st2));
-    HIPCHK(hipStreamWaitEvent(s->st, s->ev_b, 0));
-  }
-  // E_{nb-2} (written by the last k_stream) minus the changes of the last two blocks
-  const double *elast = ebuf[s->nb & 1];
-  const int sa = s->nb >= 2 ? (s->nb - 2) % 3 : -1, sb = (s->nb - 1) % 3;
+  // E_{nb-2} (written by the last k_stream) minus the changes of the last two blocks; the
+  // fused sweep has already applied them and written eps
+  const double *elast = fused ? d.eps : ebuf[s->nb & 1];
+  const int sa = (!fused && s->nb >= 2) ? (s->nb - 2) % 3 : -1, sb = fused ? -1 : (s->nb - 1) % 3;
   if (sharded) {
     if (!s->ex_eps || !s->ex_stats) { set_error("exchange buffers not set"); return -1; }
     Dev dx = d;
@@ -440,40 +450,10 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, s->device);
   const int cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-  // Two queues for the lag-1 pipeline: k_solve(s) on one reserved CU overlaps k_stream(s+1)
-  // on the others.  The reservation guarantees the solver a CU while streaming workgroups wait
-  // on its device counters.  Without CU masks both kernels share one queue (same results).
-  {
-    const char *single = getenv("BRR_SINGLE_QUEUE");
-    bool ok = false;
-    if (!(single && single[0] == '1') && cus >= 2) {
-      std::vector<uint32_t> ma((size_t)(cus + 31) / 32, 0), mb((size_t)(cus + 31) / 32, 0);
-      for (int c = 0; c < cus; ++c) {
-        if (c == 0) mb[0] |= 1u;
-        else ma[(size_t)c / 32] |= 1u << (c % 32);
-      }
-      ok = hipExtStreamCreateWithCUMask(&s->st, (uint32_t)ma.size(), ma.data()) == hipSuccess &&
-           hipExtStreamCreateWithCUMask(&s->st2, (uint32_t)mb.size(), mb.data()) == hipSuccess;
-      if (!ok) {
-        if (s->st) (void)hipStreamDestroy(s->st);
-        if (s->st2) (void)hipStreamDestroy(s->st2);
-        s->st = s->st2 = nullptr;
-      }
-    }
-    if (!ok) {
-      if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) {
-        set_error("cannot create a stream on HIP device %d", s->device);
-        delete s;
-        return nullptr;
-      }
-      s->st2 = s->st;
-    }
-    if (hipEventCreateWithFlags(&s->ev_a, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&s->ev_b, hipEventDisableTiming) != hipSuccess) {
-      set_error("cannot create events on HIP device %d", s->device);
-      delete s;
-      return nullptr;
-    }
+  if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) {
+    set_error("cannot create a stream on HIP device %d", s->device);
+    delete s;
+    return nullptr;
   }
   s->N = N; s->M = M; s->M_total = M_total; s->col_offset = col_offset;
   s->K = K; s->G = groups; s->F = (int)F; s->B = B; s->model = model;
@@ -490,7 +470,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   d.NG = (d.RG + STREAM_GROUP - 1) / STREAM_GROUP;
   const int NGpad = (d.NG + 31) / 32 * 32;  // k_solve reads slab2 in unconditional batches of 32
   const int NC = B >= 128 ? B / 128 : 1;
-  (void)cus;
+  d.gtarget = d.NG * NC;
   d.MRG = (int)((M + 255) / 256);
   const int64_t RGrows = (N + 255) / 256;
   int rc = 0;
@@ -519,13 +499,13 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   rc |= s->alloc(&d.bsz, s->nb);
   rc |= s->alloc(&d.gblk, s->nb);
   rc |= s->alloc(&d.blkorder, s->nb);
-  d.slab1_stride = (int64_t)d.RG * B;
+  d.slab1_stride = (int64_t)(d.RG + 1) * B;  // per-block: RG row tiles; fused: 2 nsg <= RG + 1 slices
   d.slab2_stride = (int64_t)NGpad * B;
   d.pend_stride = B + 16;
   rc |= s->alloc(&d.slab1, 2 * d.slab1_stride);
   rc |= s->alloc(&d.slab2, 2 * d.slab2_stride);
   rc |= s->alloc(&d.cnt1, 2 * (int64_t)d.NG * NC);
-  rc |= s->alloc(&d.gdone, 2);
+  rc |= s->alloc(&d.sync, SY_WORDS);
   rc |= s->alloc(&d.pend_idx, 3 * d.pend_stride);
   rc |= s->alloc(&d.pend_gi, 3 * d.pend_stride);
   rc |= s->alloc(&d.pend_bo, 3 * d.pend_stride);
@@ -545,7 +525,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   // every buffer a kernel may read before writing is zeroed here (recycled device memory
   // holds the previous session's values): slab2 pad rows, member padding, pending list
   bool ok = hipMemsetAsync(d.cnt1, 0, sizeof(int) * 2 * d.NG * NC, s->st) == hipSuccess &&
-            hipMemsetAsync(d.gdone, 0, sizeof(int) * 2, s->st) == hipSuccess &&
+            hipMemsetAsync(d.sync, 0, sizeof(int) * SY_WORDS, s->st) == hipSuccess &&
             hipMemsetAsync(d.pend_gi, 0, sizeof(int) * 3 * d.pend_stride, s->st) == hipSuccess &&
             hipMemsetAsync(d.pend_n, 0, sizeof(int) * 3, s->st) == hipSuccess &&
             hipMemsetAsync(d.eps, 0, sizeof(double) * d.ld, s->st) == hipSuccess &&
@@ -570,6 +550,14 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     if (s->alloc(&ga, M)) { delete s; return nullptr; }
     (void)hipMemsetAsync(ga, 0, sizeof(int) * M, s->st);
     d.gAssign = ga;
+  }
+  // fused persistent sweep (one workgroup per CU, all resident); BRR_PER_BLOCK=1 forces the
+  // per-block kernels, BRR_STREAM_WG=n caps the streaming workgroups (tests: several row tiles
+  // per half-workgroup)
+  {
+    const char *pb = getenv("BRR_PER_BLOCK");
+    const char *cap = getenv("BRR_STREAM_WG");
+    if (!(pb && pb[0] == '1') && !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused)) s->fused = FusedCfg{};
   }
   s->ref_order.resize((size_t)M);
   for (int64_t i = 0; i < M; ++i) s->ref_order[(size_t)i] = (int32_t)i;
@@ -910,7 +898,7 @@ int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
     case 100: *out = (double)sc.n_slow; return 0;     // diagnostics (not in brr.h)
     case 101: *out = (double)sc.n_changed; return 0;
     case 102: *out = (double)sc.prof_on; return 0;
-    case 103: *out = s->st2 != s->st ? 2.0 : 1.0; return 0;  // queues used by the sweep pipeline
+    case 104: *out = (double)s->fused.nsg; return 0;  // fused sweep: streaming workgroups (0 = per-block)
     case 110: case 111: case 112: case 113: case 114: case 115: case 116: case 117: case 118: case 119:
     case 120: case 121:
       *out = (double)sc.prof[which - 110]; return 0;

@@ -273,7 +273,7 @@ def main():
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (on-device Binomial(2,f) genotypes, standardised; f32 X, f64 arithmetic)",
             "config": {"workload": cfg["workload"], "N": N, "P": P, "K": K, "groups": G,
-                       "block_size": Bsz, "order": "blocked", "queues": int(s.scalar(103)), "parallelism": f"column-shard x{world}",
+                       "block_size": Bsz, "order": "blocked", "fused_stream_wg": int(s.scalar(104)), "parallelism": f"column-shard x{world}",
                        "setup_s": round(t_setup, 2), "diag": diag},
             "roofline": roof, "cpu_baseline": cpu,
         }

@@ -125,19 +125,27 @@ def test_v2_large_blocks(brr, oracle_mod, require_gpu, B):
         _compare(s, orc, O, L, L.MODEL_V2, tag=f"B={B} it={it}")
 
 
-def test_single_queue_pipeline(brr, oracle_mod, require_gpu, monkeypatch):
-    """Without CU-masked queues the stream / solve kernels share one queue in dependency order
-    (same device protocol, nothing waits): identical results to the oracle."""
+@pytest.mark.parametrize("mode", ["persistent", "persistent-multitile", "per-block"])
+def test_pipeline_modes_midsize(brr, oracle_mod, require_gpu, monkeypatch, mode):
+    """The sweep pipeline at a size with many streaming workgroups and reduction groups: the fused
+    persistent sweep (one row tile per half-workgroup, then 7 workgroups whose halves own ~6
+    tiles each) and the per-block kernels, all against the oracle over several sweeps."""
     from bayesrrcpp_amd import _lib as L
     O = oracle_mod
-    monkeypatch.setenv("BRR_SINGLE_QUEUE", "1")
-    X, Y, _ = _cohort(O, 290, 700, n_causal=30)
-    s, orc = _make(brr, O, L.MODEL_V2, X, Y, 0, B=128)
-    assert s.scalar(103) == 1.0
+    if mode == "persistent-multitile":
+        monkeypatch.setenv("BRR_STREAM_WG", "7")
+    if mode == "per-block":
+        monkeypatch.setenv("BRR_PER_BLOCK", "1")
+    X, Y, _ = _cohort(O, 20000, 3000, n_causal=60)
+    s, orc = _make(brr, O, L.MODEL_V2, X, Y, 0, B=512)
+    if mode.startswith("persistent"):
+        assert s.scalar(104) == (7 if mode == "persistent-multitile" else ((20000 + 255) // 256 + 1) // 2)
+    else:
+        assert s.scalar(104) == 0
     for it in range(4):
         s.sweep(1)
         orc.sweep(1)
-        _compare(s, orc, O, L, L.MODEL_V2, tag=f"single queue it={it}")
+        _compare(s, orc, O, L, L.MODEL_V2, tag=f"{mode} it={it}")
 
 
 def test_horseshoe_block512(brr, oracle_mod, require_gpu):
