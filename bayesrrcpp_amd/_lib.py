@@ -61,10 +61,11 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise BrrError(f"{LIB_PATH} is missing: build it with bayesrrcpp_amd.build.build_library() "
+    path = os.environ.get("BRR_LIB", LIB_PATH)  # alternative in-tree build (kernel variants)
+    if not os.path.exists(path):
+        raise BrrError(f"{path} is missing: build it with bayesrrcpp_amd.build.build_library() "
                        "(the MI355X sampler has no CPU fallback)")
-    L = C.CDLL(LIB_PATH)
+    L = C.CDLL(path)
     vp = C.c_void_p
     L.brr_options_default.argtypes = [C.POINTER(Options)]
     L.brr_last_error.restype = C.c_char_p

@@ -33,19 +33,23 @@ def _stale(target: str, deps: list[str]) -> bool:
     return any(os.path.getmtime(p) > t for p in deps)
 
 
-def build_library(force: bool = False, verbose: bool = False) -> str:
+def build_library(force: bool = False, verbose: bool = False, out: str | None = None,
+                  defines: list[str] | None = None) -> str:
+    """Build libbrr.so (or a kernel variant at `out` with extra -D `defines`)."""
+    target = out or LIB_PATH
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     deps.append(os.path.join(REPO, "include", "brr.h"))
-    if not force and not _stale(LIB_PATH, deps):
-        return LIB_PATH
+    if not force and not _stale(target, deps):
+        return target
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-o", LIB_PATH + ".tmp"] + [os.path.join(CSRC, f) for f in SOURCES] + [
+           "-Wall", "-o", target + ".tmp"] + [f"-D{x}" for x in (defines or [])] + [
+        os.path.join(CSRC, f) for f in SOURCES] + [
         "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-lpthread"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    os.replace(target + ".tmp", target)
+    return target
 
 
 def build_oracle() -> str | None:

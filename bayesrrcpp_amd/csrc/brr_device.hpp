@@ -1,7 +1,8 @@
 // brr_device.hpp -- data layout shared by the HIP kernels and the host session.
 //
 // HBM layout (one session = one GPU = one column shard):
-//   X        f32, column-major, ld = roundup(N, 64) rows (256-B aligned columns); the only
+//   X        f32, column-major, ld = roundup(N, 256) rows (1-KiB aligned columns, zero rows
+//            beyond N, so a streaming row tile never leaves the allocation); the only
 //            large array: streamed once per sweep by k_stream.
 //   eps,eps2 f64 [ld] residual (Y - mu - X beta), double-buffered across k_stream launches.
 //   beta,xsq f64 [M]; comp int32 [M]; sel uint8 [M] (marker selected a component this sweep)

@@ -888,6 +888,43 @@ __device__ __forceinline__ double wave_reduce16(double (&v)[16], int lane) {
   const double a = v[0] + __shfl_xor(v[0], 2);
   return a + __shfl_xor(a, 1);
 }
+// 8-column wave transpose-reduction: lanes with (lane & 7) == 0 hold column reduce8_col(lane)
+__device__ __forceinline__ double wave_reduce8(double (&v)[8], int lane) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const bool hi = lane & 32;
+    const double send = hi ? v[j] : v[j + 4];
+    const double keep = hi ? v[j + 4] : v[j];
+    v[j] = keep + __shfl_xor(send, 32);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const bool hi = lane & 16;
+    const double send = hi ? v[j] : v[j + 2];
+    const double keep = hi ? v[j + 2] : v[j];
+    v[j] = keep + __shfl_xor(send, 16);
+  }
+  {
+    const bool hi = lane & 8;
+    const double send = hi ? v[0] : v[1];
+    const double keep = hi ? v[1] : v[0];
+    v[0] = keep + __shfl_xor(send, 8);
+  }
+  double a = v[0] + __shfl_xor(v[0], 4);
+  a = a + __shfl_xor(a, 2);
+  return a + __shfl_xor(a, 1);
+}
+__device__ __forceinline__ int reduce8_col(int lane) {
+  return ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
+}
+
+// 16-B load through a global (address space 1) pointer: global_load_dwordx4 with an SGPR base
+typedef float v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldg4(const float *p) {
+  const v4f v = *(const __attribute__((address_space(1))) v4f *)(p);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // column held (lanes with (lane & 3) == 0) after wave_reduce16
 __device__ __forceinline__ int reduce16_col(int lane) {
   return ((lane >> 5) & 1) * 8 + ((lane >> 4) & 1) * 4 + ((lane >> 3) & 1) * 2 + ((lane >> 2) & 1);
@@ -1289,6 +1326,12 @@ __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it, int ns
 // are issued before the current item is consumed, so HBM stays busy while a workgroup waits.
 // At the end it applies the last two blocks' changes and writes eps back.
 constexpr int SWEEP_NT = 512;
+#ifndef STREAM_CW
+#define STREAM_CW 16  // columns per streaming item and wave
+#endif
+#ifndef STREAM_P
+#define STREAM_P 1    // items in flight ahead of the one being consumed (2+ spills at CW = 16)
+#endif
 constexpr int FUSED_GROUP = 8;  // streaming workgroups per level-2 reduction group
 
 __device__ __forceinline__ void apply_pending_half(const Dev &d, int slot, int tile0, int nth, double *eps_h,
@@ -1334,7 +1377,7 @@ __device__ __forceinline__ void apply_pending_half(const Dev &d, int slot, int t
   __syncthreads();
 }
 
-template <int CW>
+template <int CW, int P>
 __device__ __forceinline__ void stream_role(const Dev &d, int g, int nsg, int tmax, double *s_eps, int *s_pidx,
                                             double *s_pbo, double *s_pbn, int *s_np, int *s_last) {
 #pragma clang fp contract(off)
@@ -1357,20 +1400,26 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int nsg, int tm
   const int items = NCH * tmax; // (chunk, tile) items per wave and block, same in both halves
   const int total = items * nb;
   const int grp = g / FUSED_GROUP, gw0 = grp * FUSED_GROUP, gsz = min(FUSED_GROUP, nsg - gw0);
+  // X rows [tile * 256, +256) of a column are always inside the allocation (ld is a multiple
+  // of 256, zero rows beyond N): a wave-uniform column base plus a 16-B lane offset, no clamps.
+  // Padding tiles (k >= nth) re-read the first tile (their residual is 0).
   auto issue = [&](int it, float4 (&x)[CW]) {
     const int s = it / items, rem = it - s * items;
     const int c = rem / tmax, k = rem - c * tmax;
-    const int64_t row0 = (int64_t)(tile0 + k) * SROWS + 4 * lane;
-    const float *Xr = d.X + ((k < nth && row0 < d.N) ? row0 : 0);  // padding tiles: eps = 0
+    const int tile = __builtin_amdgcn_readfirstlane(k < nth ? tile0 + k : tile0);
+    const float *base = d.X + (int64_t)tile * SROWS;
     const int *mem = d.member + (int64_t)s * B + wh * CPW + c * CW;  // wave-uniform: scalar loads
 #pragma unroll
-    for (int j = 0; j < CW; ++j) x[j] = *reinterpret_cast<const float4 *>(Xr + (int64_t)mem[j] * ld);
+    for (int j = 0; j < CW; ++j) x[j] = ldg4(base + (int64_t)mem[j] * ld + 4 * lane);
   };
-  float4 xa[CW], xb[CW];
+  // register ring of P + 1 items: item it + P is issued before item it is consumed
+  float4 xq[P + 1][CW];
   double v[CW];
 #pragma unroll
   for (int j = 0; j < CW; ++j) v[j] = 0.0;
-  if (total > 0) issue(0, xa);
+#pragma unroll
+  for (int q = 0; q < P; ++q)
+    if (q < total) issue(q, xq[q]);
   for (int it = 0; it < total; ++it) {
     const int s = it / items, rem = it - s * items;
     const int c = rem / tmax, k = rem - c * tmax;
@@ -1379,23 +1428,33 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int nsg, int tm
       if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + s - 1, d.sync, 2);
       apply_pending_half(d, (s - 2) % 3, tile0, nth, eps_h, s_pidx, s_pbo, s_pbn, s_np);
     }
-    // prefetch the next item (possibly the next block's first) before consuming this one
-    if (it + 1 < total) issue(it + 1, xb);
+    // prefetch P items ahead (across block boundaries) before consuming this one
+    if (it + P < total) issue(it + P, xq[P]);
     const double *e = eps_h + k * SROWS + 4 * lane;
     const double e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
 #pragma unroll
     for (int j = 0; j < CW; ++j)
-      v[j] += (((double)xa[j].x * e0 + (double)xa[j].y * e1) + (double)xa[j].z * e2) + (double)xa[j].w * e3;
+      v[j] += (((double)xq[0][j].x * e0 + (double)xq[0][j].y * e1) + (double)xq[0][j].z * e2) + (double)xq[0][j].w * e3;
 #pragma unroll
-    for (int j = 0; j < CW; ++j) xa[j] = xb[j];
+    for (int q = 0; q < P; ++q)
+#pragma unroll
+      for (int j = 0; j < CW; ++j) xq[q][j] = xq[q + 1][j];
     if (k == tmax - 1) {
       // chunk done over this half's tiles: wave-reduce its CW columns
-      const double r = wave_reduce16(v, lane);
+      double r;
+      int lcol;
+      if constexpr (CW == 8) {
+        r = wave_reduce8(v, lane);
+        lcol = reduce8_col(lane);
+      } else {
+        r = wave_reduce16(v, lane);
+        lcol = reduce16_col(lane);
+      }
 #pragma unroll
       for (int j = 0; j < CW; ++j) v[j] = 0.0;
       const int par = s & 1;
-      const int col = wh * CPW + c * CW + reduce16_col(lane);
-      if ((lane & 3) == 0) st_sc1(d.slab1 + par * d.slab1_stride + (int64_t)vg * B + col, r);
+      const int col = wh * CPW + c * CW + lcol;
+      if ((lane & (64 / CW - 1)) == 0) st_sc1(d.slab1 + par * d.slab1_stride + (int64_t)vg * B + col, r);
       if (c == NCH - 1) {
         // block done: level-2 reduction over the group's row slices, then publish
         const double *slab1 = d.slab1 + par * d.slab1_stride;
@@ -1430,6 +1489,14 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int nsg, int tm
 }
 
 template <bool HS, int B>
+__device__ __forceinline__ void solver_role(const Dev &d, uint32_t it, int nslot, char *smem) {
+  for (int s = 0; s < d.nb; ++s) {
+    solve_block<HS, B, SWEEP_NT>(d, s, it, nslot, smem);
+    __syncthreads();
+  }
+}
+
+template <bool HS, int B>
 __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int nslot, int nsg, int tmax) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_last, s_np;
@@ -1442,13 +1509,10 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
   }
   __syncthreads();
   if (blockIdx.x == 0) {
-    for (int s = 0; s < d.nb; ++s) {
-      solve_block<HS, B, SWEEP_NT>(d, s, it, nslot, smem);
-      __syncthreads();
-    }
+    solver_role<HS, B>(d, it, nslot, smem);
   } else {
-    stream_role<16>(d, (int)blockIdx.x - 1, nsg, tmax, reinterpret_cast<double *>(smem), s_pidx, s_pbo, s_pbn,
-                    &s_np, &s_last);
+    stream_role<STREAM_CW, STREAM_P>(d, (int)blockIdx.x - 1, nsg, tmax, reinterpret_cast<double *>(smem), s_pidx,
+                                      s_pbo, s_pbn, &s_np, &s_last);
   }
 }
 

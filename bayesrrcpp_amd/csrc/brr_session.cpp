@@ -462,7 +462,8 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   s->nb = (int)((M + B - 1) / B);
   s->NS = stats_size(groups, K);
   Dev &d = s->d;
-  d.N = N; d.ld = (N + 63) / 64 * 64; d.M = M; d.M_total = M_total; d.col_offset = col_offset;
+  d.N = N; d.M = M; d.M_total = M_total; d.col_offset = col_offset;
+  d.ld = (N + SROWS - 1) / SROWS * SROWS;  // every streaming row tile inside the allocation (zero rows)
   d.K = K; d.G = groups; d.F = (int)F; d.B = B; d.nb = s->nb; d.model = model;
   // streaming geometry: row tiles of SROWS rows (k_stream), NC = B/128 column chunks
   d.R = SROWS;
@@ -939,9 +940,20 @@ int64_t brr_session_get_vector(brr_session *s, int32_t which, double *out) {
     case BRR_SIGMAGG: case BRR_BETAACUM: n = s->G; break;
     case BRR_PI: case BRR_VCOUNT: n = (int64_t)s->G * s->K; break;
     case BRR_ALPHA: n = s->F; break;
+    case 200: n = s->M; break;  // diagnostics: column sums of the device X (not in brr.h)
     default: set_error("unknown vector %d", which); return -1;
   }
   if (!out) return n;
+  if (which == 200) {
+    std::vector<float> x((size_t)(s->d.ld * s->M));
+    if (int rc = d2h(s, x.data(), s->d.X, (int64_t)x.size())) return rc;
+    for (int64_t j = 0; j < s->M; ++j) {
+      double a = 0;
+      for (int64_t i = 0; i < s->d.ld; ++i) a += std::fabs((double)x[(size_t)(j * s->d.ld + i)]);
+      out[j] = a;
+    }
+    return n;
+  }
   int rc = 0;
   switch (which) {
     case BRR_BETA: rc = d2h(s, out, s->d.beta, n); break;

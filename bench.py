@@ -262,6 +262,7 @@ def main():
         diag["solve_refresh_us"] = round(s.scalar(118) / calls / 100.0, 3)
         diag["solve_correct_us"] = round(s.scalar(119) / calls / 100.0, 3)
         diag["solve_wait_us"] = round(s.scalar(120) / calls / 100.0, 3)
+
         s.set_scalar(102, 0.0)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
