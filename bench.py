@@ -51,12 +51,13 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10,
+                    help="untimed sweeps (burn-in: the first sweeps from beta = 0 change ~25%% of markers)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--P", type=int, default=None)
-    ap.add_argument("--block-size", type=int, default=128)
+    ap.add_argument("--block-size", type=int, default=512)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--data-seed", type=int, default=20261015)
     ap.add_argument("--profile-solve", action="store_true", help="k_solve phase timers (diag)")
@@ -104,6 +105,21 @@ def cpu_baseline_child(args):
     o.sweep(args.cpu_sweeps)
     dt = time.perf_counter() - t0
     print(json.dumps({"t_sweep_sample_s": dt / args.cpu_sweeps, "markers": Pm, "N": N}))
+
+
+def pmc_traffic(args, N, P, B, fused):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary of the
+    same configuration (profiles/*_pmc.json: FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), or None."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if (d.get("config") == args.config and d.get("block_size") == B and fused
+                and d.get("algorithmic_bytes_per_launch") == 4.0 * N * P):
+            return d["hbm_bytes_per_launch"], os.path.relpath(f, REPO)
+    return None, None
 
 
 def cpu_baseline(args, P_full):
@@ -223,18 +239,34 @@ def main():
     # the session stream, over a few instrumented sweeps after the timed region
     roof = None
     if not args.no_roofline_events:
+        # roofline of the dominant kernel, timed with HIP events on the session stream over two
+        # instrumented sweeps after the timed region.  Fused mode: k_sweep is ONE launch per
+        # sweep that streams this shard's whole X once (algorithmic bytes 4 N P); per-block mode:
+        # k_stream streams one block (4 N B) per launch.
+        fused = s.scalar(104) > 0
         s.set_timing(True)
         s.sweep(2)
         tm = s.timing()
         s.set_timing(False)
-        avg_ms = tm["stream_ms"] / max(1, tm["stream_launches"])
-        bytes_launch = 4.0 * N * Bsz  # algorithmic: one f32 read of the block's B columns
+        nbl = (Pl + Bsz - 1) // Bsz
+        if fused:
+            launches = max(1, tm["stream_launches"] // nbl)
+            bytes_launch = 4.0 * N * Pl
+            kname = "k_sweep (fused marker loop: streaming + solver workgroups)"
+        else:
+            launches = max(1, tm["stream_launches"])
+            bytes_launch = 4.0 * N * Bsz
+            kname = "k_stream"
+        avg_ms = tm["stream_ms"] / launches
         achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(args, N, Pl, Bsz, fused)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": "k_stream", "avg_launch_us": round(avg_ms * 1e3, 3),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_source": traffic_src,
+                "kernel": kname, "avg_launch_us": round(avg_ms * 1e3, 3),
                 "bytes_per_launch": int(bytes_launch),
-                "solve_avg_us": round(tm["solve_ms"] / max(1, tm["solve_launches"]) * 1e3, 3),
+                "per_block_us": round(tm["stream_ms"] / max(1, tm["stream_launches"]) * 1e3, 3),
                 "sweep_hbm_gbs": round(4.0 * N * Pl / (ms * 1e-3) / 1e9, 1)}
     if args.trace_sweeps:
         # per-sweep wall time and changed markers of a fresh chain's first sweeps (diagnostic)
