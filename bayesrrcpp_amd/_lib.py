@@ -137,7 +137,7 @@ def check(rc: int, what: str) -> int:
     return rc
 
 
-def options(device=0, block_size=128, order_mode=ORDER_BLOCKED, shard_rank=0, shard_count=1,
+def options(device=0, block_size=0, order_mode=ORDER_BLOCKED, shard_rank=0, shard_count=1,
             verbose=0, log=None) -> Options:
     o = Options()
     lib().brr_options_default(C.byref(o))

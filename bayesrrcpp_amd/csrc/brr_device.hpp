@@ -97,6 +97,7 @@ struct Dev {
   double *mslab;
   int *mcnt;
   double *stats;
+  unsigned long long *trace;  // diagnostics: [nb][16] wall-clock events of the last traced sweep
   Scal *sc;
 };
 

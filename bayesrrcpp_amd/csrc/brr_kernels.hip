@@ -19,6 +19,7 @@
 // Everything is double precision except X, which is stored as f32 (products are exact in
 // f64).  No FMA contraction where the reference's elementwise arithmetic is restated.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 
 #include <algorithm>
@@ -144,6 +145,19 @@ __device__ __forceinline__ bool last_arriver_wt(int *cnt, int total, int *lds_fl
   }
   __syncthreads();
   return *lds_flag != 0;
+}
+
+// Diagnostics (prof_on): per-block wall-clock events of the fused sweep, Dev::trace[s][16].
+// "first" events store ~t with atomicMax (the host inverts them).
+enum TraceEv : int {
+  TR_SOLVE0 = 0, TR_GDONE_SEEN = 1, TR_CHAIN = 2, TR_PUB = 3, TR_PEND_FIRST = 4, TR_PEND_LAST = 5,
+  TR_APPLY_LAST = 6, TR_ITEMS_LAST = 7, TR_L2_LAST = 8, TR_L2_FIRST = 9, TR_ITEMS_FIRST = 10
+};
+__device__ __forceinline__ void tr_last(const Dev &d, int s, int ev) {
+  atomicMax(d.trace + (int64_t)s * 16 + ev, (unsigned long long)wall_clock64());
+}
+__device__ __forceinline__ void tr_first(const Dev &d, int s, int ev) {
+  atomicMax(d.trace + (int64_t)s * 16 + ev, ~(unsigned long long)wall_clock64());
 }
 
 // ------------------------------------------------------------------------------------
@@ -1119,7 +1133,57 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   //    between are committed as they are.  A position found outside its window is re-decided
   //    at its current num (wave-uniform) and re-examined.  A visited position's new beta is
   //    computed wave-uniformly and every later position subtracts G_ji * delta.
-  if (t < 64) {
+  if (HS && t < 64) {
+    // Horseshoe: every position changes (beta ~ N(num/D, sigmaE/D), HorseshoeR.cpp:226-234), so
+    // the chain is a forward substitution through the block in position order.  The owner lane
+    // of position j forms beta_j, the wave reads delta_j back from it and every later position
+    // subtracts G_jk delta_j -- the same operations, in the same order, as the general chain.
+    // The next step's Gram values are gathered one step ahead, off the dependency chain.
+    double r[NS], dsl[NS], sdz[NS], bo[NS], gn[NS];
+    int gg[NS];
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      const int pos = lane * NS + q;
+      const bool in = pos < bs;
+      r[q] = in ? Lr0[pos] : 0.0;
+      dsl[q] = in ? Ldsel[pos] : 1.0;
+      sdz[q] = in ? Lsdz[pos] : 0.0;
+      bo[q] = in ? Lbo[pos] : 0.0;
+      gg[q] = in ? Lgi[pos] : 0;
+    }
+    const double *Ggl = d.gram + (int64_t)gb * B * B;
+    auto row_of = [&](int j) {
+      const int sl = Lslot[j];
+      return sl >= 0 ? (const double *)(slots + (int64_t)sl * B) : Ggl + (int64_t)Lgi[j] * B;
+    };
+    {
+      const double *g0 = row_of(0);
+#pragma unroll
+      for (int q = 0; q < NS; ++q) gn[q] = g0[gg[q]];
+    }
+    for (int j = 0; j < bs; ++j) {
+      const int L = j / NS, qf = j - L * NS;
+      double gc[NS];
+#pragma unroll
+      for (int q = 0; q < NS; ++q) gc[q] = gn[q];
+      if (j + 1 < bs) {
+        const double *g1 = row_of(j + 1);
+#pragma unroll
+        for (int q = 0; q < NS; ++q) gn[q] = g1[gg[q]];
+      }
+      double rv = r[0], dv = dsl[0], zv = sdz[0], bv = bo[0];
+#pragma unroll
+      for (int q = 1; q < NS; ++q)
+        if (qf == q) { rv = r[q]; dv = dsl[q]; zv = sdz[q]; bv = bo[q]; }
+      const double bn = rv / dv + zv;  // HorseshoeR.cpp:234
+      const double delta = readlane_f64(bn - bv, L);
+      if (lane == L) Lbn[j] = bn;
+#pragma unroll
+      for (int q = 0; q < NS; ++q)
+        if (lane * NS + q > j) r[q] = r[q] - gc[q] * delta;
+    }
+    if (prof && lane == 0) atomicAdd(&d.sc->prof[6], (unsigned long long)bs);
+  } else if (!HS && t < 64) {
     double r[NS], lo[NS], hi[NS];
     int gg[NS];
     uint32_t act = 0, win = 0, valid = 0;
@@ -1293,6 +1357,8 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     if (npend) atomicAdd(&d.sc->n_changed, (unsigned long long)npend);
     if (prof) {
       const uint64_t tp4 = wall_clock64();
+      unsigned long long *tr = d.trace + (int64_t)s * 16;
+      tr[TR_SOLVE0] = tp0; tr[TR_GDONE_SEEN] = tw; tr[TR_CHAIN] = tp3; tr[TR_PUB] = tp4;
       atomicAdd(&d.sc->prof[0], (unsigned long long)(tp1 - tw));
       atomicAdd(&d.sc->prof[1], (unsigned long long)(tp2 - tp1));
       atomicAdd(&d.sc->prof[2], (unsigned long long)(tp3 - tp2));
@@ -1312,33 +1378,40 @@ __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it, int ns
 
 // ------------------------------------------------------------------------------------
 // k_sweep: the whole marker loop of a sweep in ONE persistent launch.  Workgroup 0 is the
-// solver (solve_block for s = 0..nb-1); workgroups 1..nsg stream.  Every workgroup has its own
-// CU (the solver's LDS needs it), all are resident (census at the start), so the device
-// counters of the lag-1 hand-over can be waited on (bounded).
+// solver (solve_block for s = 0..nb-1); workgroups 1..nsg stream; the last nred reduce.  Every
+// workgroup has its own CU (the solver's LDS needs it), all are resident (census at the
+// start), so the device counters of the lag-1 hand-over can be waited on (bounded).
 //
-// Streaming workgroup g = two halves of 256 threads; half h owns the row tiles
-// [vg RG / nvg, (vg+1) RG / nvg) of vg = 2g + h for the whole sweep and keeps their residual in
-// LDS.  Per block s it applies block s-2's changes (after the solver's counter says they are
-// published), forms the partial dots X_s^T E_{s-1} of its rows in (chunk, tile) items of CW
-// columns per wave -- both halves run the same item count, so the workgroup's barriers stay
-// uniform -- and reduces them across workgroups (groups of 8 workgroups = 16 row slices, last
-// arriver, write-through) for the solver.  The next item's X loads, across block boundaries,
-// are issued before the current item is consumed, so HBM stays busy while a workgroup waits.
-// At the end it applies the last two blocks' changes and writes eps back.
+// Streaming workgroup g owns the rows [g rpw, min(N, (g+1) rpw)) for the whole sweep (rpw a
+// multiple of 4, so every workgroup has the same work) and keeps their residual in LDS, in
+// npass passes of 256 rows (lane = 4 consecutive rows, 16-B loads).  Its 8 waves split the
+// block's columns (B/8 each).  Per block s it applies block s-2's changes (after the solver's
+// counter says they are published), forms the partial dots X_s^T E_{s-1} of its rows in
+// (chunk, pass) items of CW columns per wave and publishes them (one slab row per workgroup,
+// one arrival per block on its group's counter).  The next item's X loads, across block
+// boundaries, are issued before the current item is consumed, so HBM stays busy while a
+// workgroup waits.  At the end it applies the last two blocks' changes and writes eps back.
 constexpr int SWEEP_NT = 512;
+constexpr int SWEEP_NW = SWEEP_NT / 64;
 #ifndef STREAM_CW
 #define STREAM_CW 16  // columns per streaming item and wave
 #endif
 #ifndef STREAM_P
 #define STREAM_P 1    // items in flight ahead of the one being consumed (2+ spills at CW = 16)
 #endif
-constexpr int FUSED_GROUP = 8;  // streaming workgroups per level-2 reduction group
+constexpr int FUSED_GROUP = 16;  // streaming workgroups (slab rows) per level-2 reduction group
 
-__device__ __forceinline__ void apply_pending_half(const Dev &d, int slot, int tile0, int nth, double *eps_h,
-                                                   int *s_pidx, double *s_pbo, double *s_pbn, int *s_np) {
+// Block `slot`'s change list applied to this workgroup's residual rows:
+// eps_i += x_ij b_old - x_ij b_new in list order (BayesRv2.cpp:191,243).  The rows are cut into
+// 64-row slices, one row per lane, spread over the 8 waves; each wave keeps two batches of 16
+// column loads in flight (the list is padded to a multiple of 16 with neutral entries).
+__device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0, int64_t r1, int npass,
+                                              double *eps_l, int *s_pidx, double *s_pbo, double *s_pbn,
+                                              int *s_np) {
 #pragma clang fp contract(off)
+  constexpr int AB = 16;  // columns per batch
   const int t = threadIdx.x, lane = t & 63;
-  const int wh = (t >> 6) & 3;
+  const int w = t >> 6;
   if (t < 64) {
     const int np = ld_sc1_int(d.pend_n + slot);
     const int *pidx = d.pend_idx + slot * d.pend_stride;
@@ -1352,65 +1425,73 @@ __device__ __forceinline__ void apply_pending_half(const Dev &d, int slot, int t
   }
   __syncthreads();
   const int np = *s_np;
-  for (int k = wh; k < nth; k += 4) {
-    const int64_t row0 = (int64_t)(tile0 + k) * SROWS + 4 * lane;
-    const bool valid = row0 < d.N;
-    const float *Xr = d.X + (valid ? row0 : 0);
-    double *e = eps_h + k * SROWS + 4 * lane;
-    double e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
-    for (int p0 = 0; p0 < np; p0 += 8) {
-      float4 xp[8];
+  const int64_t ld = d.ld;
+  for (int sl = w; sl < npass * 4; sl += SWEEP_NW) {
+    const int off = sl * 64 + lane;
+    const bool ok = r0 + off < r1;  // rows beyond r1 read row r0 (unconditional loads) and are not stored
+    const float *Xr = d.X + (ok ? r0 + off : r0);
+    double e = eps_l[off];
+    float xa[AB], xb[AB];
+    if (np > 0) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) xp[q] = *reinterpret_cast<const float4 *>(Xr + (int64_t)s_pidx[p0 + q] * d.ld);
+      for (int q = 0; q < AB; ++q) xa[q] = Xr[(int64_t)s_pidx[q] * ld];
+    }
+    for (int p0 = 0; p0 < np; p0 += 2 * AB) {
+      const bool more = p0 + AB < np;
+      if (more) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const double bo = s_pbo[p0 + q], bn = s_pbn[p0 + q];
-        const double a0 = xp[q].x, a1 = xp[q].y, a2 = xp[q].z, a3 = xp[q].w;
-        e0 = (e0 + a0 * bo) - a0 * bn;  // BayesRv2.cpp:191,243
-        e1 = (e1 + a1 * bo) - a1 * bn;
-        e2 = (e2 + a2 * bo) - a2 * bn;
-        e3 = (e3 + a3 * bo) - a3 * bn;
+        for (int q = 0; q < AB; ++q) xb[q] = Xr[(int64_t)s_pidx[p0 + AB + q] * ld];
+      }
+#pragma unroll
+      for (int q = 0; q < AB; ++q) {
+        const double a = xa[q];
+        e = (e + a * s_pbo[p0 + q]) - a * s_pbn[p0 + q];
+      }
+      if (!more) break;
+      if (p0 + 2 * AB < np) {
+#pragma unroll
+        for (int q = 0; q < AB; ++q) xa[q] = Xr[(int64_t)s_pidx[p0 + 2 * AB + q] * ld];
+      }
+#pragma unroll
+      for (int q = 0; q < AB; ++q) {
+        const double a = xb[q];
+        e = (e + a * s_pbo[p0 + AB + q]) - a * s_pbn[p0 + AB + q];
       }
     }
-    if (valid) { e[0] = e0; e[1] = e1; e[2] = e2; e[3] = e3; }
+    if (ok) eps_l[off] = e;
   }
   __syncthreads();
 }
 
 template <int CW, int P>
-__device__ __forceinline__ void stream_role(const Dev &d, int g, int nsg, int tmax, double *s_eps, int *s_pidx,
-                                            double *s_pbo, double *s_pbn, int *s_np, int *s_last) {
+__device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int npass, double *eps_l, int *s_pidx,
+                                            double *s_pbo, double *s_pbn, int *s_np) {
 #pragma clang fp contract(off)
   const int t = threadIdx.x, lane = t & 63;
-  const int h = t >> 8;
-  const int wh = __builtin_amdgcn_readfirstlane((t >> 6) & 3);
-  const int nvg = 2 * nsg, vg = 2 * g + h;
-  const int tile0 = (int)((int64_t)vg * d.RG / nvg), tile1 = (int)((int64_t)(vg + 1) * d.RG / nvg);
-  const int nth = tile1 - tile0;  // <= tmax
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int64_t r0 = (int64_t)g * rpw, r1 = min((int64_t)d.N, r0 + rpw);
   const int B = d.B, nb = d.nb;
   const int64_t ld = d.ld;
-  double *eps_h = s_eps + h * tmax * SROWS;
-  for (int i = t & 255; i < tmax * SROWS; i += 256) {
-    const int64_t row = (int64_t)tile0 * SROWS + i;
-    eps_h[i] = (i < nth * SROWS && row < d.N) ? d.eps[row] : 0.0;
-  }
+  const bool prof = d.sc->prof_on;
+  for (int i = t; i < npass * SROWS; i += SWEEP_NT) eps_l[i] = r0 + i < r1 ? d.eps[r0 + i] : 0.0;
   __syncthreads();
-  const int CPW = B / 4;        // columns per wave
-  const int NCH = CPW / CW;     // chunks per wave and block
-  const int items = NCH * tmax; // (chunk, tile) items per wave and block, same in both halves
+  const int CPW = B / SWEEP_NW;  // columns per wave
+  const int NCH = CPW / CW;      // chunks per wave and block
+  const int items = NCH * npass; // (chunk, pass) items per wave and block
   const int total = items * nb;
-  const int grp = g / FUSED_GROUP, gw0 = grp * FUSED_GROUP, gsz = min(FUSED_GROUP, nsg - gw0);
-  // X rows [tile * 256, +256) of a column are always inside the allocation (ld is a multiple
-  // of 256, zero rows beyond N): a wave-uniform column base plus a 16-B lane offset, no clamps.
-  // Padding tiles (k >= nth) re-read the first tile (their residual is 0).
+  const int grp = g / FUSED_GROUP;
+  // Lanes whose 4 rows start at or beyond r1 re-read the workgroup's first rows (their
+  // residual rows are 0, so they add exactly 0); rows in [N, ld) are zero padding of X.  The
+  // loads stay unconditional: a divergent branch here would turn the wave-uniform member
+  // loads into vector loads whose wait drains the prefetch ring.
   auto issue = [&](int it, float4 (&x)[CW]) {
     const int s = it / items, rem = it - s * items;
-    const int c = rem / tmax, k = rem - c * tmax;
-    const int tile = __builtin_amdgcn_readfirstlane(k < nth ? tile0 + k : tile0);
-    const float *base = d.X + (int64_t)tile * SROWS;
-    const int *mem = d.member + (int64_t)s * B + wh * CPW + c * CW;  // wave-uniform: scalar loads
+    const int c = rem / npass, p = rem - c * npass;
+    const int64_t off = r0 + p * SROWS + 4 * lane < r1 ? r0 + p * SROWS + 4 * lane : r0;
+    const float *base = d.X + off;
+    const int *mem = d.member + (int64_t)s * B + w * CPW + c * CW;  // wave-uniform: scalar loads
 #pragma unroll
-    for (int j = 0; j < CW; ++j) x[j] = ldg4(base + (int64_t)mem[j] * ld + 4 * lane);
+    for (int j = 0; j < CW; ++j) x[j] = ldg4(base + (int64_t)mem[j] * ld);
   };
   // register ring of P + 1 items: item it + P is issued before item it is consumed
   float4 xq[P + 1][CW];
@@ -1422,15 +1503,24 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int nsg, int tm
     if (q < total) issue(q, xq[q]);
   for (int it = 0; it < total; ++it) {
     const int s = it / items, rem = it - s * items;
-    const int c = rem / tmax, k = rem - c * tmax;
+    const int c = rem / npass, p = rem - c * npass;
+    const bool blk_end = rem == items - 1;
     if (rem == 0 && s >= 2) {
       // block boundary: bring the residual rows from E_{s-2} to E_{s-1} (block s-2's changes)
-      if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + s - 1, d.sync, 2);
-      apply_pending_half(d, (s - 2) % 3, tile0, nth, eps_h, s_pidx, s_pbo, s_pbn, s_np);
+      if (t == 0) {
+        wait_geq(d.sync + SY_PEND, d.sbase + s - 1, d.sync, 2);
+        if (prof) { tr_first(d, s, TR_PEND_FIRST); tr_last(d, s, TR_PEND_LAST); }
+      }
+      apply_pending(d, (s - 2) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np);
+      if (prof && t == 0) {
+        tr_last(d, s, TR_APPLY_LAST);
+        if (s == nb / 2) d.trace[(int64_t)nb * 16 + 1024 + g] = wall_clock64();  // per-workgroup probe
+      }
     }
-    // prefetch P items ahead (across block boundaries) before consuming this one
-    if (it + P < total) issue(it + P, xq[P]);
-    const double *e = eps_h + k * SROWS + 4 * lane;
+    // prefetch P items ahead (across block boundaries) before consuming this one; at a block's
+    // last item the prefetch is issued after the partial-dot stores instead (see below)
+    if (!blk_end && it + P < total) issue(it + P, xq[P]);
+    const double *e = eps_l + p * SROWS + 4 * lane;
     const double e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
 #pragma unroll
     for (int j = 0; j < CW; ++j)
@@ -1439,8 +1529,8 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int nsg, int tm
     for (int q = 0; q < P; ++q)
 #pragma unroll
       for (int j = 0; j < CW; ++j) xq[q][j] = xq[q + 1][j];
-    if (k == tmax - 1) {
-      // chunk done over this half's tiles: wave-reduce its CW columns
+    if (p == npass - 1) {
+      // chunk done over this workgroup's rows: wave-reduce its CW columns
       double r;
       int lcol;
       if constexpr (CW == 8) {
@@ -1452,39 +1542,66 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int nsg, int tm
       }
 #pragma unroll
       for (int j = 0; j < CW; ++j) v[j] = 0.0;
-      const int par = s & 1;
-      const int col = wh * CPW + c * CW + lcol;
-      if ((lane & (64 / CW - 1)) == 0) st_sc1(d.slab1 + par * d.slab1_stride + (int64_t)vg * B + col, r);
-      if (c == NCH - 1) {
-        // block done: level-2 reduction over the group's row slices, then publish
-        const double *slab1 = d.slab1 + par * d.slab1_stride;
-        int *cnt1 = d.cnt1 + par * d.NG;
-        const int use = d.gbase[par] + (s >> 1);
-        if (last_arriver_wt(cnt1 + grp, (use + 1) * gsz, s_last)) {
-          const int r0 = 2 * gw0, nr = 2 * gsz;
-          for (int cl = t; cl < B; cl += SWEEP_NT) {
-            double v16[2 * FUSED_GROUP];
-#pragma unroll
-            for (int q = 0; q < 2 * FUSED_GROUP; ++q)
-              v16[q] = q < nr ? ld_sc1(slab1 + (int64_t)(r0 + q) * B + cl) : 0.0;
-            double acc = 0.0;
-#pragma unroll
-            for (int q = 0; q < 2 * FUSED_GROUP; ++q) acc += v16[q];
-            st_sc1(d.slab2 + par * d.slab2_stride + (int64_t)grp * B + cl, acc);
-          }
-          publish_add(d.sync + SY_GDONE + 32 * par, 1);
+      const int col = w * CPW + c * CW + lcol;
+      if ((lane & (64 / CW - 1)) == 0) st_sc1(d.slab1 + (s & 1) * d.slab1_stride + (int64_t)g * B + col, r);
+    }
+    if (blk_end) {
+      // block done.  The partial-dot stores were issued before the next item's loads, so
+      // waiting until only those loads are outstanding drains the stores (vmcnt counts in
+      // issue order) without draining the prefetch; then one arrival on the group counter
+      // for the reducer workgroup.
+      asm volatile("" ::: "memory");
+      if (it + P < total) issue(it + P, xq[P - 1]);
+      if (it + P < total) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P * CW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) {
+        __hip_atomic_fetch_add(d.cnt1 + (s & 1) * d.NG + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prof) {
+          tr_first(d, s, TR_ITEMS_FIRST);
+          tr_last(d, s, TR_ITEMS_LAST);
+          if (s == nb / 2) d.trace[(int64_t)nb * 16 + g] = wall_clock64();
         }
       }
     }
   }
   // end of sweep: the last two blocks' changes, then the residual rows back to HBM
   if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + nb, d.sync, 4);
-  if (nb >= 2) apply_pending_half(d, (nb - 2) % 3, tile0, nth, eps_h, s_pidx, s_pbo, s_pbn, s_np);
+  if (nb >= 2) apply_pending(d, (nb - 2) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np);
   else __syncthreads();
-  apply_pending_half(d, (nb - 1) % 3, tile0, nth, eps_h, s_pidx, s_pbo, s_pbn, s_np);
-  for (int i = t & 255; i < nth * SROWS; i += 256) {
-    const int64_t row = (int64_t)tile0 * SROWS + i;
-    if (row < d.N) d.eps[row] = eps_h[i];
+  apply_pending(d, (nb - 1) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np);
+  for (int i = t; i < npass * SROWS; i += SWEEP_NT)
+    if (r0 + i < r1) d.eps[r0 + i] = eps_l[i];
+}
+
+// Reducer workgroup r: for every block, the level-2 sums of the groups r, r + nred, ... (the
+// partials of a group's 16 streaming workgroups, in workgroup order) into slab2, then
+// one arrival on the solver's counter.  Kept off the streaming workgroups, which go straight on
+// to the next block.
+__device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nred, bool prof) {
+  const int t = threadIdx.x;
+  const int ng = (nsg + FUSED_GROUP - 1) / FUSED_GROUP;
+  const int B = d.B;
+  for (int s = 0; s < d.nb; ++s) {
+    const int par = s & 1;
+    const int use = d.gbase[par] + (s >> 1);
+    const double *slab1 = d.slab1 + par * d.slab1_stride;
+    for (int grp = r; grp < ng; grp += nred) {
+      const int gw0 = grp * FUSED_GROUP, gsz = min(FUSED_GROUP, nsg - gw0);
+      if (t == 0) wait_geq(d.cnt1 + par * d.NG + grp, (use + 1) * gsz, d.sync, 6);
+      __syncthreads();
+      for (int cl = t; cl < B; cl += SWEEP_NT) {
+        double v16[FUSED_GROUP];
+#pragma unroll
+        for (int q = 0; q < FUSED_GROUP; ++q) v16[q] = q < gsz ? ld_sc1(slab1 + (int64_t)(gw0 + q) * B + cl) : 0.0;
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < FUSED_GROUP; ++q) acc += v16[q];
+        st_sc1(d.slab2 + par * d.slab2_stride + (int64_t)grp * B + cl, acc);
+      }
+      publish_add(d.sync + SY_GDONE + 32 * par, 1);
+      if (prof && t == 0) { tr_first(d, s, TR_L2_FIRST); tr_last(d, s, TR_L2_LAST); }
+    }
   }
 }
 
@@ -1497,22 +1614,25 @@ __device__ __forceinline__ void solver_role(const Dev &d, uint32_t it, int nslot
 }
 
 template <bool HS, int B>
-__global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int nslot, int nsg, int tmax) {
+__global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int nslot, int nsg, int rpw, int npass,
+                                                        int nred) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ int s_last, s_np;
+  __shared__ int s_np;
   __shared__ int s_pidx[BMAX + 16];
   __shared__ double s_pbo[BMAX + 16], s_pbn[BMAX + 16];
   // residency census: every workgroup must be running before any waits on another
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(d.sync + SY_ARRIVE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    wait_geq(d.sync + SY_ARRIVE, d.abase + nsg + 1, d.sync, 5);
+    wait_geq(d.sync + SY_ARRIVE, d.abase + nsg + 1 + nred, d.sync, 5);
   }
   __syncthreads();
   if (blockIdx.x == 0) {
     solver_role<HS, B>(d, it, nslot, smem);
+  } else if ((int)blockIdx.x > nsg) {
+    reduce_role(d, (int)blockIdx.x - 1 - nsg, nsg, nred, d.sc->prof_on);
   } else {
-    stream_role<STREAM_CW, STREAM_P>(d, (int)blockIdx.x - 1, nsg, tmax, reinterpret_cast<double *>(smem), s_pidx,
-                                      s_pbo, s_pbn, &s_np, &s_last);
+    stream_role<STREAM_CW, STREAM_P>(d, (int)blockIdx.x - 1, rpw, npass, reinterpret_cast<double *>(smem), s_pidx,
+                                      s_pbo, s_pbn, &s_np);
   }
 }
 
@@ -1776,8 +1896,8 @@ hipError_t launch_stream(const Dev &d, int s, const double *eps_in, double *eps_
   return hipGetLastError();
 }
 
-// Fused sweep geometry: one solver + nsg streaming workgroups, one per CU (the solver's LDS),
-// each half of a streaming workgroup owning at most tmax row tiles.  Returns false when the
+// Fused sweep geometry: one solver, nsg streaming and nred reducing workgroups, one per CU (the
+// solver's LDS), each streamer owning rpw rows (npass passes of 256).  Returns false when the
 // configuration cannot be made resident (the per-block kernels are used then).
 template <bool HS, int B>
 static const void *sweep_fn() { return (const void *)k_sweep<HS, B>; }
@@ -1793,11 +1913,23 @@ static const void *sweep_kernel(int model, int B) {
 }
 
 bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
-  if (cus < 2 || d.B % 64 != 0) return false;
-  int nsg = std::min(cus - 1, (d.RG + 1) / 2);
-  if (max_wg > 0) nsg = std::min(nsg, max_wg);
-  nsg = std::max(nsg, 1);
-  const int tmax = (d.RG + 2 * nsg - 1) / (2 * nsg);
+  // the 8 waves of a streaming workgroup split a block's columns in chunks of STREAM_CW
+  if (cus < 3 || d.B % (SWEEP_NW * STREAM_CW) != 0) return false;
+  // one CU each: the solver, nsg streamers (rows split evenly, at least 256 rows each) and
+  // nred reducers (one per group of 16 streamers)
+  const auto ngr = [](int n) { return (n + FUSED_GROUP - 1) / FUSED_GROUP; };
+  int cap = cus - 2;
+  while (cap > 1 && 1 + cap + ngr(cap) > cus) --cap;
+  if (max_wg > 0) cap = std::min(cap, max_wg);
+  cap = std::max(cap, 1);
+  const char *al = getenv("BRR_ROW_ALIGN");  // diagnostics: row-range alignment (default 4)
+  const int64_t align = al && atoi(al) >= 4 ? (atoi(al) + 3) / 4 * 4 : 4;
+  int64_t rpw = (d.N + cap - 1) / cap;
+  rpw = std::max<int64_t>(SROWS, (rpw + align - 1) / align * align);
+  const int nsg = (int)((d.N + rpw - 1) / rpw);
+  const int npass = (int)((rpw + SROWS - 1) / SROWS);
+  const int nred = ngr(nsg);
+  if (nsg > d.RG + 1) return false;  // slab1 rows
   const void *fn = sweep_kernel(d.model, d.B);
   hipFuncAttributes attr;
   if (hipFuncGetAttributes(&attr, fn) != hipSuccess) return false;
@@ -1806,7 +1938,7 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   const size_t fixed = solve_fixed_bytes(d.B, K);
   if (fixed + 8 * (size_t)d.B > budget) return false;
   const int nslot = (int)std::min<size_t>((size_t)d.B, (budget - fixed) / (8 * (size_t)d.B));
-  const size_t eps_bytes = (size_t)2 * tmax * SROWS * sizeof(double);
+  const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double);
   const size_t lds = std::max(fixed + (size_t)nslot * 8 * d.B, eps_bytes);
   if (lds > budget) return false;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) != hipSuccess) return false;
@@ -1814,18 +1946,20 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, SWEEP_NT, lds) != hipSuccess || per_cu < 1)
     return false;
   cfg->nsg = nsg;
-  cfg->tmax = tmax;
+  cfg->rpw = (int)rpw;
+  cfg->npass = npass;
   cfg->nslot = nslot;
-  cfg->ngroups = (nsg + FUSED_GROUP - 1) / FUSED_GROUP;
+  cfg->ngroups = nred;
+  cfg->nred = nred;
   cfg->lds = lds;
   return true;
 }
 
 hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipStream_t st) {
   const bool hs = d.model == MODEL_HORSESHOE;
-  const dim3 grid((unsigned)(c.nsg + 1)), blk(SWEEP_NT);
+  const dim3 grid((unsigned)(c.nsg + 1 + c.nred)), blk(SWEEP_NT);
 #define BRR_SWEEP_LAUNCH(HSV, BV) \
-  hipLaunchKernelGGL((k_sweep<HSV, BV>), grid, blk, c.lds, st, d, it, c.nslot, c.nsg, c.tmax)
+  hipLaunchKernelGGL((k_sweep<HSV, BV>), grid, blk, c.lds, st, d, it, c.nslot, c.nsg, c.rpw, c.npass, c.nred)
   switch (d.B) {
     case 64: if (hs) BRR_SWEEP_LAUNCH(true, 64); else BRR_SWEEP_LAUNCH(false, 64); break;
     case 128: if (hs) BRR_SWEEP_LAUNCH(true, 128); else BRR_SWEEP_LAUNCH(false, 128); break;

@@ -29,7 +29,7 @@ hipError_t launch_fixed(const Dev &d, uint32_t it, bool perm_on_device, hipStrea
 hipError_t launch_stream(const Dev &d, int s, const double *eps_in, double *eps_out, hipStream_t st);
 hipError_t launch_prep(const Dev &d, uint32_t it, hipStream_t st);
 struct FusedCfg {
-  int nsg = 0, tmax = 0, nslot = 0, ngroups = 0;
+  int nsg = 0, rpw = 0, npass = 0, nslot = 0, ngroups = 0, nred = 0;
   size_t lds = 0;
 };
 bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg);

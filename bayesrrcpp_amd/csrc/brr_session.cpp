@@ -274,7 +274,7 @@ int do_sweep_local(brr_session *s) {
   d.gbase[0] = s->gbase[0];
   d.gbase[1] = s->gbase[1];
   d.abase = s->abase;
-  if (s->fused.nsg > 0) s->abase += s->fused.nsg + 1;
+  if (s->fused.nsg > 0) s->abase += s->fused.nsg + 1 + s->fused.nred;
   s->sbase += s->nb;
   s->gbase[0] += (s->nb + 1) / 2;
   s->gbase[1] += s->nb / 2;
@@ -393,7 +393,7 @@ extern "C" {
 void brr_options_default(brr_options *o) {
   std::memset(o, 0, sizeof *o);
   o->abi_version = BRR_ABI_VERSION;
-  o->block_size = 128;
+  o->block_size = 0;  // automatic: 512 (BayesR family), 128 (Horseshoe)
   o->order_mode = BRR_ORDER_BLOCKED;
   o->shard_count = 1;
 }
@@ -420,7 +420,10 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   if (groups < 1 || groups > MAXG) { set_error("groups=%d outside [1,%d]", groups, MAXG); return nullptr; }
   if (model != MODEL_GROUPS) F = 0;
   if (F < 0 || F > 1024) { set_error("fixed effects F=%lld outside [0,1024]", (long long)F); return nullptr; }
-  int B = opt.block_size > 0 ? opt.block_size : 128;
+  // automatic block size: the BayesR family changes few markers per block (long blocks amortise
+  // the per-block hand-over); the Horseshoe resamples every marker, and B = 128 keeps the whole
+  // Gram block of its serial chain in LDS
+  int B = opt.block_size > 0 ? opt.block_size : (model == MODEL_HORSESHOE ? 128 : 512);
   if (B % 64 != 0 || B > BMAX) { set_error("block_size=%d must be a multiple of 64 and <= %d", B, BMAX); return nullptr; }
   if (opt.shard_count < 1) opt.shard_count = 1;
   if (opt.shard_count > 1 && (col_offset % B) != 0) {
@@ -512,6 +515,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   rc |= s->alloc(&d.pend_bo, 3 * d.pend_stride);
   rc |= s->alloc(&d.pend_bn, 3 * d.pend_stride);
   rc |= s->alloc(&d.pend_n, 3);
+  rc |= s->alloc(&d.trace, (int64_t)s->nb * 16 + 2048);  // + per-workgroup probes
   d.nbB = (int64_t)s->nb * B;
   rc |= s->alloc(&d.mc, d.nbB * (3 + 2 * std::max(K, 1)));
   rc |= s->alloc(&d.rslab, 2 * RGrows);
@@ -923,6 +927,7 @@ int brr_session_set_scalar(brr_session *s, int32_t which, double v) {
     case 102:  // diagnostics: k_solve phase timers on/off (resets the totals)
       sc.prof_on = v != 0.0;
       for (auto &x : sc.prof) x = 0;
+      HIPCHK(hipMemsetAsync(s->d.trace, 0, sizeof(unsigned long long) * (16 * (size_t)s->nb + 2048), s->st));
       break;
     default: set_error("scalar %d not settable", which); return -1;
   }
@@ -941,9 +946,16 @@ int64_t brr_session_get_vector(brr_session *s, int32_t which, double *out) {
     case BRR_PI: case BRR_VCOUNT: n = (int64_t)s->G * s->K; break;
     case BRR_ALPHA: n = s->F; break;
     case 200: n = s->M; break;  // diagnostics: column sums of the device X (not in brr.h)
+    case 201: n = (int64_t)s->nb * 16 + 2048; break;  // diagnostics: per-block event trace (brr_kernels.hip TR_*)
     default: set_error("unknown vector %d", which); return -1;
   }
   if (!out) return n;
+  if (which == 201) {
+    std::vector<unsigned long long> tr((size_t)n);
+    if (int rc = d2h(s, tr.data(), s->d.trace, n)) return rc;
+    for (int64_t i = 0; i < n; ++i) out[i] = (double)tr[(size_t)i];
+    return n;
+  }
   if (which == 200) {
     std::vector<float> x((size_t)(s->d.ld * s->M));
     if (int rc = d2h(s, x.data(), s->d.X, (int64_t)x.size())) return rc;

@@ -34,7 +34,7 @@ def _run(fn, *args):
 
 
 def BayesRSamplerV2(outputFile, seed, max_iterations, burn_in, thinning, X, Y, sigma0, v0E, s02E,
-                    v0G, s02G, cva, *, device=0, block_size=128, order_mode=L.ORDER_BLOCKED,
+                    v0G, s02G, cva, *, device=0, block_size=0, order_mode=L.ORDER_BLOCKED,
                     verbose=0, log=None):
     X = _f(X)
     Y = np.ascontiguousarray(Y, dtype=np.float64).ravel()
@@ -48,7 +48,7 @@ def BayesRSamplerV2(outputFile, seed, max_iterations, burn_in, thinning, X, Y, s
 
 
 def BayesRSamplerV2Groups(outputFile, seed, max_iterations, burn_in, thinning, X, Y, sigma0, v0E,
-                          s02E, v0G, s02G, cva, groups, gAssign, fixed, *, device=0, block_size=128,
+                          s02E, v0G, s02G, cva, groups, gAssign, fixed, *, device=0, block_size=0,
                           order_mode=L.ORDER_BLOCKED, verbose=0, log=None):
     X = _f(X)
     N, M = X.shape
@@ -67,7 +67,7 @@ def BayesRSamplerV2Groups(outputFile, seed, max_iterations, burn_in, thinning, X
 
 def BRV2Grstart(outputFile, seed, max_iterations, burn_in, thinning, mu, beta, sigmaE, sigmaGG, X,
                 epsilon, components, sigma0, v0E, s02E, v0G, s02G, cva, groups, gAssign, *,
-                device=0, block_size=128, order_mode=L.ORDER_BLOCKED, verbose=0, log=None):
+                device=0, block_size=0, order_mode=L.ORDER_BLOCKED, verbose=0, log=None):
     X = _f(X)
     N, M = X.shape
     beta = np.ascontiguousarray(beta, dtype=np.float64).ravel()
@@ -87,7 +87,7 @@ def BRV2Grstart(outputFile, seed, max_iterations, burn_in, thinning, mu, beta, s
 
 
 def HorseshoeR(outputFile, seed, max_iterations, burn_in, thinning, X, Y, A, v0E, s02E, vL, vT, c2,
-               vC, sC, *, device=0, block_size=128, order_mode=L.ORDER_BLOCKED, verbose=0, log=None):
+               vC, sC, *, device=0, block_size=0, order_mode=L.ORDER_BLOCKED, verbose=0, log=None):
     X = _f(X)
     N, M = X.shape
     Y = np.ascontiguousarray(Y, dtype=np.float64).ravel()

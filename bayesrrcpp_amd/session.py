@@ -27,7 +27,7 @@ class Session:
     """
 
     def __init__(self, model, N, M, *, K=1, groups=1, F=0, M_total=None, col_offset=0,
-                 device=0, block_size=128, order_mode=L.ORDER_BLOCKED, shard_rank=0,
+                 device=0, block_size=0, order_mode=L.ORDER_BLOCKED, shard_rank=0,
                  shard_count=1, verbose=0, log=None):
         self._keep = []
         self.model, self.N, self.M, self.K, self.G, self.F = model, N, M, K, groups, F

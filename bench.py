@@ -48,6 +48,49 @@ CONFIGS = {
 }
 
 
+def block_events(raw):
+    """Medians over the blocks of one traced sweep.  'lat_*' are measured from the solver's
+    publication of block s-2's changes, which is what streaming block s waits for."""
+    import numpy as np
+    raw = np.asarray(raw, dtype=np.float64)
+    probe = raw[-2048:].reshape(2, 1024)
+    tr = raw[:-2048].reshape(-1, 16)
+    u64 = float(2 ** 64)
+    first = lambda c: u64 - 1 - tr[:, c]  # noqa: E731  (stored as ~t)
+    nb = tr.shape[0]
+    if nb < 6:
+        return {}
+    sl = slice(4, nb - 1)
+    pub_m2 = np.roll(tr[:, 3], 2)
+    ev = {
+        "period": np.diff(tr[:, 0])[sl],
+        "solver_wait": (tr[:, 1] - tr[:, 0])[sl],
+        "solver_chain": (tr[:, 2] - tr[:, 1])[sl],
+        "solver_publish": (tr[:, 3] - tr[:, 2])[sl],
+        "lat_pend_seen_first": (first(4) - pub_m2)[sl],
+        "lat_pend_seen_last": (tr[:, 5] - pub_m2)[sl],
+        "lat_apply_last": (tr[:, 6] - pub_m2)[sl],
+        "lat_items_first": (first(10) - pub_m2)[sl],
+        "lat_items_last": (tr[:, 7] - pub_m2)[sl],
+        "lat_l2_first": (first(9) - pub_m2)[sl],
+        "lat_l2_last": (tr[:, 8] - pub_m2)[sl],
+        "lat_solver_sees": (tr[:, 1] - pub_m2)[sl],
+    }
+    out = {k: round(float(np.median(v)) / 100.0, 2) for k, v in ev.items()}
+    # per-workgroup probe of block nb/2: pend seen and items done, by XCD (blockIdx % 8)
+    done, seen = probe[0], probe[1]
+    g = np.nonzero(done)[0]
+    if len(g):
+        t0 = done[g].min()
+        xcd = (g + 1) % 8
+        out["probe_done_by_xcd"] = [round(float(np.mean(done[g][xcd == x] - t0)) / 100.0, 2) for x in range(8)]
+        out["probe_seen_by_xcd"] = [round(float(np.mean(seen[g][xcd == x] - t0)) / 100.0, 2) for x in range(8)]
+        out["probe_done_pct"] = [round(float(np.percentile(done[g] - t0, q)) / 100.0, 2) for q in (0, 10, 50, 90, 100)]
+        out["probe_busy_pct"] = [round(float(np.percentile(done[g] - seen[g], q)) / 100.0, 2) for q in (0, 10, 50, 90, 100)]
+        out["probe_slowest_wg"] = [int(x) for x in g[np.argsort(done[g] - seen[g])[-8:]]]
+    return out
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -57,7 +100,8 @@ def parse():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--P", type=int, default=None)
-    ap.add_argument("--block-size", type=int, default=512)
+    ap.add_argument("--block-size", type=int, default=0,
+                    help="marker block B; 0 = the library's automatic choice (512 BayesR family, 128 Horseshoe)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--data-seed", type=int, default=20261015)
     ap.add_argument("--profile-solve", action="store_true", help="k_solve phase timers (diag)")
@@ -167,8 +211,8 @@ def main():
     cfg = CONFIGS[args.config]
     N = args.N or cfg["N"]
     P = args.P or cfg["P"]
-    Bsz = args.block_size
     model = {"v2": L.MODEL_V2, "groups": L.MODEL_GROUPS, "hs": L.MODEL_HORSESHOE}[cfg["model"]]
+    Bsz = args.block_size or (128 if model == L.MODEL_HORSESHOE else 512)
     G = cfg["groups"]
     # contiguous block shards
     nb = (P + Bsz - 1) // Bsz
@@ -294,7 +338,11 @@ def main():
         diag["solve_refresh_us"] = round(s.scalar(118) / calls / 100.0, 3)
         diag["solve_correct_us"] = round(s.scalar(119) / calls / 100.0, 3)
         diag["solve_wait_us"] = round(s.scalar(120) / calls / 100.0, 3)
-
+        if int(s.scalar(104)) > 0:
+            # per-block event trace of one fused sweep (brr_kernels.hip TR_*), medians in us
+            s.set_scalar(102, 1.0)
+            s.sweep(1)
+            diag["block_events_us"] = block_events(s.vector(201))
         s.set_scalar(102, 0.0)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -163,7 +163,7 @@ class Oracle:
     """One oracle chain. Arrays are kept alive on the instance (C holds raw pointers)."""
 
     def __init__(self, model, X=None, Y=None, *, cva=None, gAssign=None, fixed=None, G=1,
-                 seed=1, order_mode=ORDER_BLOCKED, block_size=128, n_shards=1,
+                 seed=1, order_mode=ORDER_BLOCKED, block_size=0, n_shards=1,
                  sigma0=0.01, v0E=1e-4, s02E=1e-3, v0G=1e-4, s02G=1e-3,
                  A=1.0, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0,
                  mu0=0.0, sigmaE0=1.0, beta0=None, sigmaGG0=None, eps0=None, comp0=None,
@@ -204,7 +204,8 @@ class Oracle:
                 setattr(cfg, name, _dptr(keep(np.ascontiguousarray(arr, dtype=np.float64).ravel())))
         cfg.seed = seed
         cfg.order_mode = order_mode
-        cfg.block_size = block_size
+        # 0 = the library's automatic block size (brr_session.cpp brr_session_create)
+        cfg.block_size = block_size or (128 if model == HORSESHOE else 512)
         cfg.n_shards = n_shards
         cfg.shard_only = shard_only
         self.cfg = cfg

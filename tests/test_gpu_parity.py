@@ -125,21 +125,25 @@ def test_v2_large_blocks(brr, oracle_mod, require_gpu, B):
         _compare(s, orc, O, L, L.MODEL_V2, tag=f"B={B} it={it}")
 
 
-@pytest.mark.parametrize("mode", ["persistent", "persistent-multitile", "per-block"])
+@pytest.mark.parametrize("mode", ["persistent", "persistent-cap7", "persistent-cap30", "per-block"])
 def test_pipeline_modes_midsize(brr, oracle_mod, require_gpu, monkeypatch, mode):
     """The sweep pipeline at a size with many streaming workgroups and reduction groups: the fused
-    persistent sweep (one row tile per half-workgroup, then 7 workgroups whose halves own ~6
-    tiles each) and the per-block kernels, all against the oracle over several sweeps."""
+    persistent sweep (256 rows per streaming workgroup; 7 workgroups of 12 passes; 30 workgroups
+    of 668 rows, the last one ragged) and the per-block kernels, all against the oracle over
+    several sweeps."""
     from bayesrrcpp_amd import _lib as L
     O = oracle_mod
-    if mode == "persistent-multitile":
-        monkeypatch.setenv("BRR_STREAM_WG", "7")
+    cap = {"persistent-cap7": 7, "persistent-cap30": 30}.get(mode)
+    if cap:
+        monkeypatch.setenv("BRR_STREAM_WG", str(cap))
     if mode == "per-block":
         monkeypatch.setenv("BRR_PER_BLOCK", "1")
-    X, Y, _ = _cohort(O, 20000, 3000, n_causal=60)
+    N = 20000
+    X, Y, _ = _cohort(O, N, 3000, n_causal=60)
     s, orc = _make(brr, O, L.MODEL_V2, X, Y, 0, B=512)
     if mode.startswith("persistent"):
-        assert s.scalar(104) == (7 if mode == "persistent-multitile" else ((20000 + 255) // 256 + 1) // 2)
+        rpw = max(256, (-(-N // cap) + 3) // 4 * 4) if cap else 256
+        assert s.scalar(104) == -(-N // rpw)
     else:
         assert s.scalar(104) == 0
     for it in range(4):
@@ -264,7 +268,7 @@ def test_oneshot_csv_v2(brr, oracle_mod, require_gpu, tmp_path):
     p_orc = str(tmp_path / "orc.csv")
     brr.BayesRSamplerV2(p_gpu, 5, 30, 10, 4, X, Y, HYP["sigma0"], HYP["v0E"], HYP["s02E"],
                         HYP["v0G"], HYP["s02G"], CVA, log=lambda m: None)
-    O.run_csv(p_orc, O.V2, X, Y, 30, 10, 4, cva=CVA, seed=5, order_mode=0, block_size=128, **HYP)
+    O.run_csv(p_orc, O.V2, X, Y, 30, 10, 4, cva=CVA, seed=5, order_mode=0, **HYP)
     g = open(p_gpu).read().splitlines()
     o = open(p_orc).read().splitlines()
     assert g[0] == o[0]  # header
@@ -335,7 +339,7 @@ def test_rccl_single_rank(brr, oracle_mod, require_gpu):
     s.upload_x(X).set_y(Y).set_bayesr(**HYP, cva=CVA).init(3)
     s.comm_init(comm_unique_id(), 1, 0)
     s.sweep(3)
-    orc = O.Oracle(O.V2, X, Y, cva=CVA, seed=3, order_mode=0, block_size=128, **HYP)
+    orc = O.Oracle(O.V2, X, Y, cva=CVA, seed=3, order_mode=0, **HYP)
     orc.sweep(3)
     _compare(s, orc, O, L, L.MODEL_V2, tag="rccl 1 rank")
 
