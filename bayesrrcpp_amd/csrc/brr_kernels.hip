@@ -704,6 +704,34 @@ __device__ __forceinline__ FastDec decide_pos(const Dev &d, double r, const doub
   return o;
 }
 
+// Out-of-line copies for the serial chains' rare paths (re-decision, exact formula): inlined, their
+// MAXK-wide arrays raise the register pressure of the whole fused kernel into spills, and spill
+// reloads on the chain wait behind the streaming workgroups' HBM traffic.
+__device__ __noinline__ Decision decide_bayesr_ool(double num, double xsq, double sigmaE, double sigmaG,
+                                                   const double *pi_g, const double *cva_g, int Gs, int K, double p,
+                                                   bool want_margin) {
+  return decide_bayesr(num, xsq, sigmaE, sigmaG, pi_g, cva_g, Gs, K, p, want_margin);
+}
+// decide_pos for the chains: the fast decision inline, the exact fallback out of line
+__device__ __forceinline__ FastDec decide_pos_ool(const int *gAssign, const double *sigmaGG, const double *pi,
+                                                  const double *cva, int G, int K, double r, const double *a,
+                                                  const double *den, int64_t stride, double sigmaE, double p,
+                                                  double x2, int m) {
+  FastDec o = decide_fast(r, a, den, stride, K, sigmaE, p);
+  if (o.ex) {
+    const int g = gAssign ? gAssign[m] : 0;
+    Decision dc = decide_bayesr_ool(r, x2, sigmaE, sigmaGG[g], pi + (int64_t)g * K, cva + g, G, K, p, true);
+    if (dc.margin > 0.0) {
+      const double t = r * r;
+      o.k = dc.k;
+      o.lo = t - dc.margin;
+      o.hi = t + dc.margin;
+      o.ex = false;
+    }
+  }
+  return o;
+}
+
 // ------------------------------------------------------------------------------------
 // k_stream(s): residual update for block s-2 + partial dots of block s (lag-1 pipeline).
 // While k_solve(s-1) runs on the other queue, k_stream(s) forms d = X_s^T E_{s-1}, with E_t
@@ -966,6 +994,17 @@ constexpr size_t SOLVE_LDS_MAX = 160 * 1024;
 __host__ __device__ inline size_t solve_scratch_doubles(int B, int NT) {
   return (size_t)(B + 16) + (B + 16) / 2 + 1 + (size_t)(B < NT ? NT / B : 1) * B;
 }
+// Resident-Gram mode (B <= RESIDENT_BMAX and LDS for B + scratch rows): the whole Gram block
+// is copied into LDS during phase A (LDS-DMA, before the wait for the streaming side), the
+// slot of a row is its Gram index, the phase-A scratch moves behind the rows, and the chain
+// keeps every per-position constant in registers (solve_block step 3).
+constexpr int RESIDENT_BMAX = 128;
+__host__ __device__ inline int solve_scratch_rows(int B, int NT) {
+  return (int)((solve_scratch_doubles(B, NT) + B - 1) / B);
+}
+__host__ __device__ inline int solve_max_slots(int B, int NT) {
+  return B <= RESIDENT_BMAX ? B + solve_scratch_rows(B, NT) : B;
+}
 
 // One block position s, by one workgroup (called per launch, or in a loop by the persistent
 // solver).  Phase A needs nothing from k_stream(s): per-position constants, the previous
@@ -1015,6 +1054,224 @@ __device__ __forceinline__ void ring_produce(const double *Gblk, const int *Lgi,
   }
 }
 
+// Correctly rounded num / D on the chain: q0 = num * RN(1/D), one exact-remainder correction
+// (Markstein) -- three dependent operations instead of the division sequence.
+__device__ __forceinline__ double quot_rn(double num, double den, double inv) {
+  const double q0 = num * inv;
+  return __builtin_fma(__builtin_fma(-q0, den, num), inv, q0);
+}
+
+// Resident-Gram serial chain, Horseshoe (wave 0).  Every position changes
+// (beta ~ N(num/D, sigmaE/D), HorseshoeR.cpp:226-234): a forward substitution through the block in
+// position order.  Lane l holds positions l + 64 q and every constant of them in registers; each
+// step, every lane forms the new beta of its position in the current plane (only the owner's is
+// used), the wave reads delta from the owner, and every later position subtracts G_jk delta_j.
+template <int B>
+__device__ __forceinline__ void chain_hs_resident(int bs, const double *Lr0, const double *Ldsel, const double *Lsdz,
+                                                  const double *Lbo, double *Lbn, const int *Lgi,
+                                                  const double *slots) {
+#pragma clang fp contract(off)
+  constexpr int NS = B / 64;
+  const int lane = threadIdx.x & 63;
+  double r[NS], dv[NS], iv[NS], zv[NS], cz[NS], bn[NS];
+  int gg[NS];
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    const int pos = lane + 64 * q;
+    const bool in = pos < bs;
+    r[q] = in ? Lr0[pos] : 0.0;
+    dv[q] = in ? Ldsel[pos] : 1.0;
+    iv[q] = 1.0 / dv[q];
+    zv[q] = in ? Lsdz[pos] : 0.0;
+    bn[q] = in ? Lbo[pos] : 0.0;
+    cz[q] = zv[q] - bn[q];  // delta = num / D + (z - beta_old)
+    gg[q] = in ? Lgi[pos] : 0;
+  }
+  // Gram row of position j (lane j & 63 of plane j >> 6) gathered at this lane's positions
+  auto gather = [&](int j, double (&g)[NS]) __attribute__((always_inline)) {
+    int gi = 0;
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+      if ((j >> 6) == q) gi = __builtin_amdgcn_readlane(gg[q], j & 63);
+    const double *row = slots + (int64_t)gi * B;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) g[q] = row[gg[q]];
+  };
+  // Step j: the owner's delta from its num (3-operation quotient + one add), then
+  // r_k -= G_jk delta for k > j as one FMA with the coefficient zeroed at k <= j.  Gram
+  // values are gathered GD steps ahead into a ring of GD register sets (unrolled by GD, so a
+  // set is consumed before it is refilled and no register copy waits on a pending gather).
+  constexpr int GD = 4;
+  double gb[GD][NS];
+#pragma unroll
+  for (int u = 0; u < GD; ++u)
+    if (u < bs) gather(u, gb[u]);
+#pragma unroll
+  for (int qo = 0; qo < NS; ++qo) {
+    const int jend = min(bs, 64 * (qo + 1));
+    for (int j0 = 64 * qo; j0 < jend; j0 += GD) {
+#pragma unroll
+      for (int u = 0; u < GD; ++u) {
+        const int j = j0 + u;
+        if (j >= jend) break;
+        double gm[NS];
+#pragma unroll
+        for (int q = 0; q < NS; ++q) gm[q] = lane + 64 * q > j ? gb[u][q] : 0.0;
+        if (j + GD < bs) gather(j + GD, gb[u]);
+        const int own = j - 64 * qo;
+        const double quo = quot_rn(r[qo], dv[qo], iv[qo]);
+        const double delta = readlane_f64(quo + cz[qo], own);
+        if (lane == own) bn[qo] = quo + zv[qo];  // HorseshoeR.cpp:234
+#pragma unroll
+        for (int q = qo; q < NS; ++q) r[q] = __builtin_fma(-gm[q], delta, r[q]);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NS; ++q)
+    if (lane + 64 * q < bs) Lbn[lane + 64 * q] = bn[q];
+}
+
+// Resident-Gram serial chain, BayesR family (wave 0).  Lane l holds positions l NS .. l NS + NS-1
+// with their current num (r), decision window [lo, hi] in num^2, chosen component and its
+// constants in registers.  The next position to visit is the lowest one that is predicted to
+// change (act), needs the exact formula (ex) or whose num^2 left its window; every lane forms
+// the new beta of its own lowest candidate in parallel with the wave's search, so a fast step
+// is: ballot -> owner lane -> read delta -> update the later positions from the LDS Gram row.
+// A position found outside its window is re-decided at its current num (wave-uniform) and
+// re-examined; an exact-formula position is evaluated by decide_bayesr (BayesRv2.cpp:195-242).
+template <int B>
+__device__ __forceinline__ void chain_bayesr_resident(const Dev &d, int bs, double sigmaE, const double *Lr0,
+                                                      const double *Llo, const double *Lhi, const double *Ldsel,
+                                                      const double *Lsdz, const double *Lbo, double *Lbn,
+                                                      const int *Lfl, int *Lks, const int *Lgi, const double *La,
+                                                      const double *Lden, const double *Lp, const double *Lx2,
+                                                      const double *Lz, const int *Lm, const double *slots,
+                                                      bool prof) {
+#pragma clang fp contract(off)
+  constexpr int NS = B / 64;
+  constexpr uint32_t ALLQ = (1u << NS) - 1u;
+  const int lane = threadIdx.x & 63;
+  double r[NS], lo[NS], hi[NS], dv[NS], iv[NS], sz[NS], bo[NS], bn[NS];
+  int gg[NS], ks[NS];
+  uint32_t act = 0, win = 0, valid = 0, exb = 0;
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    const int pos = lane * NS + q;
+    const bool in = pos < bs;
+    const int fl = in ? Lfl[pos] : 0;
+    r[q] = in ? Lr0[pos] : 0.0;
+    lo[q] = in ? Llo[pos] : 1.0;
+    hi[q] = in ? Lhi[pos] : -1.0;
+    dv[q] = in ? Ldsel[pos] : 1.0;
+    iv[q] = 1.0 / dv[q];
+    sz[q] = in ? Lsdz[pos] : 0.0;
+    bo[q] = in ? Lbo[pos] : 0.0;
+    bn[q] = bo[q];
+    gg[q] = in ? Lgi[pos] : 0;
+    ks[q] = fl & 0xFF;
+    const double tt = r[q] * r[q];
+    valid |= (uint32_t)in << q;
+    act |= (uint32_t)(in && (fl & PF_LIKELY)) << q;
+    exb |= (uint32_t)(in && (fl & PF_EX)) << q;
+    win |= (uint32_t)(in && tt >= lo[q] && tt <= hi[q]) << q;
+  }
+  int nslow = 0, nsteps = 0, nref = 0;
+  int i = 0;
+  uint64_t tslow = 0;
+  const uint64_t tl0 = prof ? wall_clock64() : 0;
+  while (true) {
+    const int lowq = min(max(i - lane * NS, 0), NS);
+    const uint32_t ge = ALLQ & ~((1u << lowq) - 1u);
+    const uint32_t cand = valid & (act | ~win | exb) & ge;
+    const int ql = cand ? __builtin_ctz(cand) : 0;
+    double rv = r[0], dvv = dv[0], ivv = iv[0], szv = sz[0], bov = bo[0];
+    int ksv = ks[0], ggv = gg[0];
+#pragma unroll
+    for (int q = 1; q < NS; ++q)
+      if (ql == q) { rv = r[q]; dvv = dv[q]; ivv = iv[q]; szv = sz[q]; bov = bo[q]; ksv = ks[q]; ggv = gg[q]; }
+    // speculative new beta of this lane's lowest candidate (BayesRv2.cpp:226-230)
+    const double bnl = ksv == 0 ? 0.0 : (ksv == FALLTHROUGH ? bov : quot_rn(rv, dvv, ivv) + szv);
+    const int fastl = (int)(((win & ~exb) >> ql) & 1u);
+    const uint64_t bal = __ballot(cand != 0);
+    if (!bal) break;  // the rest keep their decisions (no change)
+    const int L = __builtin_ctzll(bal);
+    const int qf = __builtin_amdgcn_readlane(ql, L);
+    const int first = L * NS + qf;  // wave-uniform
+    const double *grow = slots + (int64_t)__builtin_amdgcn_readlane(ggv, L) * B;
+    double delta;
+    if (__builtin_amdgcn_readlane(fastl, L)) {
+      delta = readlane_f64(bnl - bov, L);
+      if (lane == L) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q)
+          if (q == qf) bn[q] = bnl;
+      }
+    } else {
+      const uint64_t ts0 = prof ? wall_clock64() : 0;
+      const double rf = readlane_f64(rv, L);
+      const bool exf = (__builtin_amdgcn_readlane((int)exb, L) >> qf) & 1;
+      if (!exf) {
+        // outside its window: re-decide at the current num, then re-examine
+        FastDec o = decide_pos_ool(d.gAssign, d.sigmaGG, d.pi, d.cva, d.G, d.K, rf, La + first, Lden + first, B, sigmaE, Lp[first], Lx2[first], Lm[first]);
+        const bool lk = o.ex || !(o.k == FALLTHROUGH || (o.k == 0 && readlane_f64(bov, L) == 0.0));
+        const double dsel = (!o.ex && o.k >= 1 && o.k != FALLTHROUGH) ? Lden[(o.k - 1) * B + first] : 1.0;
+        const double sdz = sqrt(sigmaE / dsel) * Lz[first];
+        if (lane == L) {
+#pragma unroll
+          for (int q = 0; q < NS; ++q)
+            if (q == qf) { lo[q] = o.lo; hi[q] = o.hi; ks[q] = o.k; dv[q] = dsel; iv[q] = 1.0 / dsel; sz[q] = sdz; }
+          act = (act & ~(1u << qf)) | ((uint32_t)lk << qf);
+          win = (win & ~(1u << qf)) | ((uint32_t)(!o.ex) << qf);
+          exb = (exb & ~(1u << qf)) | ((uint32_t)o.ex << qf);
+        }
+        ++nref;
+        if (prof) tslow += wall_clock64() - ts0;
+        continue;
+      }
+      const double bof = readlane_f64(bov, L);
+      const int m = Lm[first];
+      const int g = d.gAssign ? d.gAssign[m] : 0;
+      Decision dc = decide_bayesr_ool(rf, Lx2[first], sigmaE, d.sigmaGG[g], d.pi + (int64_t)g * d.K, d.cva + g, d.G,
+                                      d.K, Lp[first], false);
+      const double bnf = dc.k == 0 ? 0.0 : (dc.k == FALLTHROUGH ? bof : rf / dc.denom + sqrt(sigmaE / dc.denom) * Lz[first]);
+      if (lane == L) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q)
+          if (q == qf) { bn[q] = bnf; ks[q] = dc.k; }
+      }
+      delta = bnf - bof;
+      ++nslow;
+      if (prof) tslow += wall_clock64() - ts0;
+    }
+    if (delta != 0.0) {
+#pragma unroll
+      for (int q = 0; q < NS; ++q) {
+        const int pos = lane * NS + q;
+        if (pos > first && pos < bs) {
+          r[q] = r[q] - grow[gg[q]] * delta;
+          const double tt = r[q] * r[q];
+          win = (win & ~(1u << q)) | ((uint32_t)(tt >= lo[q] && tt <= hi[q]) << q);
+        }
+      }
+    }
+    i = first + 1;
+    ++nsteps;
+  }
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    const int pos = lane * NS + q;
+    if (pos < bs) { Lbn[pos] = bn[q]; Lks[pos] = ks[q]; }
+  }
+  if (lane == 0 && nslow) atomicAdd(&d.sc->n_slow, (unsigned long long)nslow);
+  if (prof && lane == 0) {
+    atomicAdd(&d.sc->prof[6], (unsigned long long)nsteps);
+    atomicAdd(&d.sc->prof[7], (unsigned long long)nref);
+    atomicAdd(&d.sc->prof[8], (unsigned long long)tslow);                  // solve_refresh_us: slow paths
+    atomicAdd(&d.sc->prof[9], (unsigned long long)(wall_clock64() - tl0));  // solve_correct_us: whole loop
+  }
+}
+
 template <bool HS, int B, int NT>
 __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, int nslot, char *smem) {
 #pragma clang fp contract(off)
@@ -1040,6 +1297,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   const double sigmaE = d.sc->sigmaE;
   const int64_t S = d.nbB;
   const int64_t q0 = (int64_t)s * B;
+  const bool resident = B <= RESIDENT_BMAX && nslot >= B + solve_scratch_rows(B, NT);
 
   // A) everything that does not depend on k_stream(s)
   const double *C = nullptr;
@@ -1087,9 +1345,10 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   // thread groups take contiguous parts of the list and their partial sums are added in group
   // order.
   constexpr int PG = B < NT ? NT / B : 1;
-  double *Lcd = slots;
-  int *Lcg = reinterpret_cast<int *>(slots + (B + 16));
-  double *Lpart = slots + (B + 16) + (B + 16) / 2 + 1;
+  double *scr = resident ? slots + (int64_t)B * B : slots;
+  double *Lcd = scr;
+  int *Lcg = reinterpret_cast<int *>(scr + (B + 16));
+  double *Lpart = scr + (B + 16) + (B + 16) / 2 + 1;
   for (int e = t; e < np_prev; e += NT) {
     Lcg[e] = ld_sc1_int(pv_gi + e);
     Lcd[e] = ld_sc1(pv_bn + e) - ld_sc1(pv_bo + e);
@@ -1127,10 +1386,22 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       Lr0[t] = corr;
     }
   }
+  if (resident) {
+    // the whole Gram block into the slot area (row gi at slots + gi B) by LDS-DMA, 1 KiB per
+    // wave-instruction; issued after phase A's own loads were consumed, so the copy is in
+    // flight during the wait below and retired by the barrier that follows it
+    constexpr int NCHUNK = B * B * 8 / 1024;
+    const char *src = reinterpret_cast<const char *>(d.gram + (int64_t)gb * B * B);
+    char *dst = reinterpret_cast<char *>(slots);
+    for (int c = wv; c < NCHUNK; c += NW)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + c * 1024 + lane * 16),
+                                       (__attribute__((address_space(3))) void *)(dst + c * 1024), 16, 0, 0);
+  }
   // B) wait for k_stream(s)'s reduction groups (other queue; cumulative count)
   if (t == 0 && s == 0) stamp(d.sync, 3);
   if (t == 0) wait_geq(d.sync + SY_GDONE + 32 * par, (d.gbase[par] + (s >> 1) + 1) * d.gtarget, d.sync, 3);
   if (t == 0 && s == 0) stamp(d.sync, 4);
+  if (resident) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces landed
   __syncthreads();
   if (prof) tw = wall_clock64();
   const double *slab2 = d.slab2 + par * d.slab2_stride;
@@ -1193,7 +1464,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     for (int w = 0; w < NW; ++w) base += misc[w];
     __syncthreads();
   }
-  const int nused = min(base, nst);
+  const int nused = resident ? 0 : min(base, nst);  // resident: every row is in LDS already
   const int nov = max(base - nst, 0);  // predicted positions served by the ring
   if (t == 0) {
     *Lcons = 0;
@@ -1220,6 +1491,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   }
   __syncthreads();
   if (prof) tp2 = wall_clock64();
+  const uint64_t tc2 = prof ? __builtin_amdgcn_s_memtime() : 0;  // shader clock (diagnostics)
   // 3) serial chain on wave 0; lane l owns positions l*NS .. l*NS+NS-1.  Per position: the
   //    current num (r), its decision window [lo, hi] in num^2, and two bits: act (the decision
   //    changes beta, or needs the exact formula) and win (num^2 inside the window).  The next
@@ -1227,7 +1499,17 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   //    between are committed as they are.  A position found outside its window is re-decided
   //    at its current num (wave-uniform) and re-examined.  A visited position's new beta is
   //    computed wave-uniformly and every later position subtracts G_ji * delta.
-  if (HS && t < 64) {
+  if (resident) {
+    if (t < 64) {
+      if constexpr (HS) {
+        chain_hs_resident<B>(bs, Lr0, Ldsel, Lsdz, Lbo, Lbn, Lgi, slots);
+        if (prof && lane == 0) atomicAdd(&d.sc->prof[6], (unsigned long long)bs);
+      } else {
+        chain_bayesr_resident<B>(d, bs, sigmaE, Lr0, Llo, Lhi, Ldsel, Lsdz, Lbo, Lbn, Lfl, Lks, Lgi, La, Lden, Lp,
+                                 Lx2, Lz, Lm, slots, prof);
+      }
+    }
+  } else if (HS && t < 64) {
     // Horseshoe: every position changes (beta ~ N(num/D, sigmaE/D), HorseshoeR.cpp:226-234), so
     // the chain is a forward substitution through the block in position order.  The owner lane
     // of position j forms beta_j, the wave reads delta_j back from it and every later position
@@ -1345,7 +1627,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       if (!HS && !exf && !winf) {
         // re-decide `first` at its current num (wave-uniform), then re-examine it
         const uint64_t tr0 = prof ? wall_clock64() : 0;
-        FastDec o = decide_pos(d, rf, La + first, Lden + first, B, sigmaE, Lp[first], Lx2[first], Lm[first]);
+        FastDec o = decide_pos_ool(d.gAssign, d.sigmaGG, d.pi, d.cva, d.G, d.K, rf, La + first, Lden + first, B, sigmaE, Lp[first], Lx2[first], Lm[first]);
         const double bo = Lbo[first];
         const bool lk = o.ex || !(o.k == FALLTHROUGH || (o.k == 0 && bo == 0.0));
         const double dsel = (!o.ex && o.k >= 1 && o.k != FALLTHROUGH) ? Lden[(o.k - 1) * B + first] : 1.0;
@@ -1375,8 +1657,8 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       } else if (exf) {
         const int m = Lm[first];
         const int g = d.gAssign ? d.gAssign[m] : 0;
-        Decision dc = decide_bayesr(rf, Lx2[first], sigmaE, d.sigmaGG[g], d.pi + (int64_t)g * d.K, d.cva + g, d.G,
-                                    d.K, Lp[first], false);
+        Decision dc = decide_bayesr_ool(rf, Lx2[first], sigmaE, d.sigmaGG[g], d.pi + (int64_t)g * d.K, d.cva + g, d.G,
+                                        d.K, Lp[first], false);
         ks = dc.k;
         bn = dc.k == 0 ? 0.0 : (dc.k == FALLTHROUGH ? bof : rf / dc.denom + sqrt(sigmaE / dc.denom) * Lz[first]);
         ++nslow;
@@ -1435,6 +1717,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   }
   __syncthreads();
   if (prof) tp3 = wall_clock64();
+  const uint64_t tc3 = prof ? __builtin_amdgcn_s_memtime() : 0;
   // 4) write back, compact the changed markers into this block's list (position order)
   const int pslot = s % 3;
   int *pidx = d.pend_idx + pslot * d.pend_stride, *pgi = d.pend_gi + pslot * d.pend_stride;
@@ -1499,6 +1782,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       atomicAdd(&d.sc->prof[3], (unsigned long long)(tp4 - tp3));
       atomicAdd(&d.sc->prof[5], 1ull);
       atomicAdd(&d.sc->prof[10], (unsigned long long)(tw - tp0));
+      atomicAdd(&d.sc->prof[11], (unsigned long long)(tc3 - tc2));
     }
   }
 }
@@ -1752,8 +2036,6 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
                                                         int nred) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_np;
-  __shared__ int s_pidx[BMAX + 16];
-  __shared__ double s_pbo[BMAX + 16], s_pbn[BMAX + 16];
   // residency census: every workgroup must be running before any waits on another
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(d.sync + SY_ARRIVE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1765,8 +2047,11 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
   } else if ((int)blockIdx.x > nsg) {
     reduce_role(d, (int)blockIdx.x - 1 - nsg, nsg, nred, d.sc->prof_on);
   } else {
-    stream_role<STREAM_CW, STREAM_P>(d, (int)blockIdx.x - 1, rpw, npass, reinterpret_cast<double *>(smem), s_pidx,
-                                      s_pbo, s_pbn, &s_np);
+    // streamer LDS: residual rows, then the change list being applied (stream_lds_bytes)
+    double *eps_l = reinterpret_cast<double *>(smem);
+    double *s_pbo = eps_l + (int64_t)npass * SROWS, *s_pbn = s_pbo + (d.B + 16);
+    int *s_pidx = reinterpret_cast<int *>(s_pbn + (d.B + 16));
+    stream_role<STREAM_CW, STREAM_P>(d, (int)blockIdx.x - 1, rpw, npass, eps_l, s_pidx, s_pbo, s_pbn, &s_np);
   }
 }
 
@@ -2073,9 +2358,10 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   const int K = d.model == MODEL_HORSESHOE ? 1 : d.K;
   const size_t fixed = solve_fixed_bytes(d.B, K);
   if (fixed + 8 * (size_t)d.B > budget) return false;
-  const int nslot = (int)std::min<size_t>((size_t)d.B, (budget - fixed) / (8 * (size_t)d.B));
+  const int nslot = (int)std::min<size_t>((size_t)solve_max_slots(d.B, SWEEP_NT), (budget - fixed) / (8 * (size_t)d.B));
   if ((size_t)nslot * d.B < solve_scratch_doubles(d.B, SWEEP_NT)) return false;
-  const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double);
+  // streamers: residual rows + the change list (indices, old and new betas) in LDS
+  const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double) + (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int));
   const size_t lds = std::max(fixed + (size_t)nslot * 8 * d.B, eps_bytes);
   if (lds > budget) return false;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) != hipSuccess) return false;
@@ -2120,7 +2406,8 @@ hipError_t launch_prep(const Dev &d, uint32_t it, hipStream_t st) {
 static int solve_slots(int B, int K) {
   const size_t fixed = solve_fixed_bytes(B, K);
   const int n = (int)((SOLVE_LDS_MAX - fixed) / (8 * (size_t)B));
-  return n < B ? n : B;
+  const int mx = solve_max_slots(B, 256);
+  return n < mx ? n : mx;
 }
 
 size_t solve_lds_bytes(int B, int K) { return solve_fixed_bytes(B, K) + (size_t)solve_slots(B, K) * 8 * B; }
