@@ -1063,9 +1063,14 @@ __device__ __forceinline__ double quot_rn(double num, double den, double inv) {
 
 // Resident-Gram serial chain, Horseshoe (wave 0).  Every position changes
 // (beta ~ N(num/D, sigmaE/D), HorseshoeR.cpp:226-234): a forward substitution through the block in
-// position order.  Lane l holds positions l + 64 q and every constant of them in registers; each
-// step, every lane forms the new beta of its position in the current plane (only the owner's is
-// used), the wave reads delta from the owner, and every later position subtracts G_jk delta_j.
+// position order,
+//     delta_j = (num_j - sum_{i<j} G_ij delta_i) / D_j + (z_j - beta_old_j).
+// Lane l holds positions l + 64 q in registers as the scaled quantity
+//     s_j = num_j / D_j + (z_j - beta_old_j) - sum_{i<j, visited} (G_ij / D_j) delta_i,
+// which IS delta_j when position j is reached: a step is one read of the owner's s_j and one FMA
+// per later position with the pre-scaled coefficient G_ij / D_j (zero at positions <= j).  The
+// dependency chain per step is readlane + FMA; the Gram values are gathered GD steps ahead and
+// scaled off the chain.  beta_new = beta_old + delta (same value as num/D + z up to rounding).
 template <int B>
 __device__ __forceinline__ void chain_hs_resident(int bs, const double *Lr0, const double *Ldsel, const double *Lsdz,
                                                   const double *Lbo, double *Lbn, const int *Lgi,
@@ -1073,18 +1078,18 @@ __device__ __forceinline__ void chain_hs_resident(int bs, const double *Lr0, con
 #pragma clang fp contract(off)
   constexpr int NS = B / 64;
   const int lane = threadIdx.x & 63;
-  double r[NS], dv[NS], iv[NS], zv[NS], cz[NS], bn[NS];
+  double sv[NS], iv[NS], bo[NS];
   int gg[NS];
 #pragma unroll
   for (int q = 0; q < NS; ++q) {
     const int pos = lane + 64 * q;
     const bool in = pos < bs;
-    r[q] = in ? Lr0[pos] : 0.0;
-    dv[q] = in ? Ldsel[pos] : 1.0;
-    iv[q] = 1.0 / dv[q];
-    zv[q] = in ? Lsdz[pos] : 0.0;
-    bn[q] = in ? Lbo[pos] : 0.0;
-    cz[q] = zv[q] - bn[q];  // delta = num / D + (z - beta_old)
+    const double dv = in ? Ldsel[pos] : 1.0;
+    iv[q] = 1.0 / dv;
+    bo[q] = in ? Lbo[pos] : 0.0;
+    const double r = in ? Lr0[pos] : 0.0;
+    const double z = in ? Lsdz[pos] : 0.0;
+    sv[q] = quot_rn(r, dv, iv[q]) + (z - bo[q]);
     gg[q] = in ? Lgi[pos] : 0;
   }
   // Gram row of position j (lane j & 63 of plane j >> 6) gathered at this lane's positions
@@ -1097,10 +1102,10 @@ __device__ __forceinline__ void chain_hs_resident(int bs, const double *Lr0, con
 #pragma unroll
     for (int q = 0; q < NS; ++q) g[q] = row[gg[q]];
   };
-  // Step j: the owner's delta from its num (3-operation quotient + one add), then
-  // r_k -= G_jk delta for k > j as one FMA with the coefficient zeroed at k <= j.  Gram
-  // values are gathered GD steps ahead into a ring of GD register sets (unrolled by GD, so a
-  // set is consumed before it is refilled and no register copy waits on a pending gather).
+  // ring of GD gathered rows, unrolled by GD: a set is consumed before it is refilled.  The
+  // scheduling barrier at the end of each step keeps the gather GD steps ahead of its use (the
+  // machine scheduler otherwise sinks it next to the use and the step waits for the LDS
+  // latency: 84 -> ~31 cycles per step on an idle GPU, scripts/mb_chain.hip)
   constexpr int GD = 4;
   double gb[GD][NS];
 #pragma unroll
@@ -1114,22 +1119,20 @@ __device__ __forceinline__ void chain_hs_resident(int bs, const double *Lr0, con
       for (int u = 0; u < GD; ++u) {
         const int j = j0 + u;
         if (j >= jend) break;
-        double gm[NS];
+        double h[NS];
 #pragma unroll
-        for (int q = 0; q < NS; ++q) gm[q] = lane + 64 * q > j ? gb[u][q] : 0.0;
+        for (int q = 0; q < NS; ++q) h[q] = lane + 64 * q > j ? gb[u][q] * iv[q] : 0.0;
         if (j + GD < bs) gather(j + GD, gb[u]);
-        const int own = j - 64 * qo;
-        const double quo = quot_rn(r[qo], dv[qo], iv[qo]);
-        const double delta = readlane_f64(quo + cz[qo], own);
-        if (lane == own) bn[qo] = quo + zv[qo];  // HorseshoeR.cpp:234
+        const double delta = readlane_f64(sv[qo], j - 64 * qo);
 #pragma unroll
-        for (int q = qo; q < NS; ++q) r[q] = __builtin_fma(-gm[q], delta, r[q]);
+        for (int q = qo; q < NS; ++q) sv[q] = __builtin_fma(-h[q], delta, sv[q]);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
   }
 #pragma unroll
   for (int q = 0; q < NS; ++q)
-    if (lane + 64 * q < bs) Lbn[lane + 64 * q] = bn[q];
+    if (lane + 64 * q < bs) Lbn[lane + 64 * q] = bo[q] + sv[q];  // HorseshoeR.cpp:234
 }
 
 // Resident-Gram serial chain, BayesR family (wave 0).  Lane l holds positions l NS .. l NS + NS-1
@@ -1919,6 +1922,8 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
 #pragma unroll
   for (int q = 0; q < P; ++q)
     if (q < total) issue(q, xq[q]);
+  // diagnostics (prof): this workgroup's accumulated wait / apply / streaming time of the sweep
+  uint64_t acc_wait = 0, acc_apply = 0, acc_stream = 0, t_mark = prof ? wall_clock64() : 0;
   for (int it = 0; it < total; ++it) {
     const int s = it / items, rem = it - s * items;
     const int c = rem / npass, p = rem - c * npass;
@@ -1927,12 +1932,21 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       // block boundary: bring the residual rows from E_{s-2} to E_{s-1} (block s-2's changes)
       if (t == 0) {
         wait_geq(d.sync + SY_PEND, d.sbase + s - 1, d.sync, 2);
-        if (prof) { tr_first(d, s, TR_PEND_FIRST); tr_last(d, s, TR_PEND_LAST); }
+        if (prof) {
+          tr_first(d, s, TR_PEND_FIRST);
+          tr_last(d, s, TR_PEND_LAST);
+          const uint64_t tn = wall_clock64();
+          acc_wait += tn - t_mark;
+          t_mark = tn;
+        }
       }
       apply_pending(d, (s - 2) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np);
       if (prof && t == 0) {
         tr_last(d, s, TR_APPLY_LAST);
         if (s == nb / 2) d.trace[(int64_t)nb * 16 + 1024 + g] = wall_clock64();  // per-workgroup probe
+        const uint64_t tn = wall_clock64();
+        acc_apply += tn - t_mark;
+        t_mark = tn;
       }
     }
     // prefetch P items ahead (across block boundaries) before consuming this one; at a block's
@@ -1979,9 +1993,18 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
           tr_first(d, s, TR_ITEMS_FIRST);
           tr_last(d, s, TR_ITEMS_LAST);
           if (s == nb / 2) d.trace[(int64_t)nb * 16 + g] = wall_clock64();
+          const uint64_t tn = wall_clock64();
+          acc_stream += tn - t_mark;
+          t_mark = tn;
         }
       }
     }
+  }
+  if (prof && t == 0) {
+    unsigned long long *acc = d.trace + (int64_t)nb * 16 + 2048;
+    acc[g] = acc_wait;
+    acc[1024 + g] = acc_apply;
+    acc[2048 + g] = acc_stream;
   }
   // end of sweep: the last two blocks' changes, then the residual rows back to HBM
   if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + nb, d.sync, 4);

@@ -53,8 +53,10 @@ def block_events(raw):
     publication of block s-2's changes, which is what streaming block s waits for."""
     import numpy as np
     raw = np.asarray(raw, dtype=np.float64)
-    probe = raw[-2048:].reshape(2, 1024)
-    tr = raw[:-2048].reshape(-1, 16)
+    nbk = (raw.size - 5120) // 16
+    tr = raw[:nbk * 16].reshape(-1, 16)
+    probe = raw[nbk * 16:nbk * 16 + 2048].reshape(2, 1024)
+    acc = raw[nbk * 16 + 2048:].reshape(3, 1024)  # per streaming workgroup: wait, apply, stream
     u64 = float(2 ** 64)
     first = lambda c: u64 - 1 - tr[:, c]  # noqa: E731  (stored as ~t)
     nb = tr.shape[0]
@@ -88,6 +90,16 @@ def block_events(raw):
         out["probe_done_pct"] = [round(float(np.percentile(done[g] - t0, q)) / 100.0, 2) for q in (0, 10, 50, 90, 100)]
         out["probe_busy_pct"] = [round(float(np.percentile(done[g] - seen[g], q)) / 100.0, 2) for q in (0, 10, 50, 90, 100)]
         out["probe_slowest_wg"] = [int(x) for x in g[np.argsort(done[g] - seen[g])[-8:]]]
+    # whole-sweep totals per streaming workgroup (ms): systematic vs random imbalance
+    busy = acc[1] + acc[2]
+    w = np.nonzero(busy)[0]
+    if len(w):
+        ms = lambda v: [round(float(x) / 1e5, 3) for x in v]  # noqa: E731  (100 MHz ticks)
+        out["wg_wait_ms_pct"] = ms(np.percentile(acc[0][w], [0, 10, 50, 90, 100]))
+        out["wg_apply_ms_pct"] = ms(np.percentile(acc[1][w], [0, 10, 50, 90, 100]))
+        out["wg_stream_ms_pct"] = ms(np.percentile(acc[2][w], [0, 10, 50, 90, 100]))
+        out["wg_busy_by_xcd_ms"] = ms([np.mean(busy[w][(w + 1) % 8 == x]) for x in range(8)])
+        out["wg_slowest"] = [int(x) for x in w[np.argsort(busy[w])[-8:]]]
     return out
 
 
