@@ -13,6 +13,7 @@ from .build import LIB_PATH
 
 MODEL_V2, MODEL_GROUPS, MODEL_RESTART, MODEL_HORSESHOE = 0, 1, 2, 3
 ORDER_BLOCKED, ORDER_REFERENCE, ORDER_IDENTITY = 0, 1, 2
+X_F32, X_2BIT = 0, 1  # brr_x_storage
 (MU, SIGMAE, SIGMAG, SIGMAF, TAU, ETA, C2, SUMSQ_BETA) = range(8)
 (BETA, COMP, EPS, SIGMAGG, PI, ALPHA, LAMBDA, XSQ, ORDER, VCOUNT, BETAACUM, HSV) = range(12)
 ABI_VERSION = 1
@@ -28,7 +29,7 @@ class Options(C.Structure):
     _fields_ = [
         ("abi_version", C.c_int32), ("device", C.c_int32), ("block_size", C.c_int32),
         ("order_mode", C.c_int32), ("shard_rank", C.c_int32), ("shard_count", C.c_int32),
-        ("verbose", C.c_int32), ("reserved0", C.c_int32),
+        ("verbose", C.c_int32), ("x_storage", C.c_int32),
         ("log", LOG_FN), ("log_userdata", C.c_void_p),
     ]
 
@@ -38,7 +39,7 @@ EXPORTED = [
     "brr_options_default", "brr_last_error", "brr_device_count",
     "brr_BayesRSamplerV2", "brr_BayesRSamplerV2Groups", "brr_BRV2Grstart", "brr_HorseshoeR",
     "brr_session_create", "brr_session_destroy", "brr_session_upload_x_f64",
-    "brr_session_upload_x_f32", "brr_session_synthesize", "brr_session_synth_partial_y",
+    "brr_session_upload_x_f32", "brr_session_upload_bed", "brr_session_synthesize", "brr_session_synth_partial_y",
     "brr_session_synth_y", "brr_session_set_y",
     "brr_session_set_fixed", "brr_session_set_bayesr", "brr_session_set_horseshoe",
     "brr_session_set_restart", "brr_session_set_pi", "brr_session_init", "brr_session_sweep",
@@ -90,6 +91,7 @@ def lib():
     L.brr_session_destroy.argtypes = [vp]
     L.brr_session_upload_x_f64.argtypes = [vp, D, C.c_int64]
     L.brr_session_upload_x_f32.argtypes = [vp, C.POINTER(C.c_float), C.c_int64]
+    L.brr_session_upload_bed.argtypes = [vp, C.POINTER(C.c_uint8), C.c_int64]
     L.brr_session_synthesize.argtypes = [vp, C.c_uint64, C.c_double, C.c_int64]
     L.brr_session_synth_partial_y.argtypes = [vp, D]
     L.brr_session_synth_y.argtypes = [vp, D, C.c_uint64, C.c_double]
@@ -138,11 +140,12 @@ def check(rc: int, what: str) -> int:
 
 
 def options(device=0, block_size=0, order_mode=ORDER_BLOCKED, shard_rank=0, shard_count=1,
-            verbose=0, log=None) -> Options:
+            verbose=0, log=None, x_storage=X_F32) -> Options:
     o = Options()
     lib().brr_options_default(C.byref(o))
     o.device, o.block_size, o.order_mode = device, block_size, order_mode
     o.shard_rank, o.shard_count, o.verbose = shard_rank, shard_count, verbose
+    o.x_storage = x_storage
     if log is not None:
         cb = LOG_FN(lambda msg, _u: log(msg.decode()))
         o.log = cb

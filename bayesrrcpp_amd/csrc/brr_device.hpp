@@ -4,6 +4,10 @@
 //   X        f32, column-major, ld = roundup(N, 256) rows (1-KiB aligned columns, zero rows
 //            beyond N, so a streaming row tile never leaves the allocation); the only
 //            large array: streamed once per sweep by k_stream.
+//   Xc+xlut  alternative genotype storage: 2-bit codes, column-major, ld/4 bytes
+//            per column (PLINK .bed packing), and a 4-entry f32 value table per column.  The
+//            decoded values are the f32 values the X storage would hold, so every kernel
+//            computes on bit-identical inputs; a sweep reads N P / 4 bytes instead of 4 N P.
 //   eps,eps2 f64 [ld] residual (Y - mu - X beta), double-buffered across k_stream launches.
 //   beta,xsq f64 [M]; comp int32 [M]; sel uint8 [M] (marker selected a component this sweep)
 //   gram     f64 [nb][B][B] block Gram matrices X_b^T X_b of the fixed column blocks.
@@ -72,7 +76,11 @@ struct Dev {
   int gtarget;      // reduction groups k_solve(s) waits for (per-block: NG * NC; persistent: NG)
   uint64_t seed;
   Hyper hyp;
-  const float *X;
+  const float *X;      // f32 storage (x_storage BRR_X_F32), else nullptr
+  const uint8_t *Xc;   // 2-bit genotype codes (BRR_X_2BIT), else nullptr: column j at Xc + j ldc,
+                       // row i in bits 2(i&3)..2(i&3)+1 of byte i>>2 (PLINK .bed packing)
+  const float *xlut;   // [M][4] value of each code of column j (padding rows decode to 0)
+  int64_t ldc;         // bytes per code column = ld / 4
   const double *Y, *fixed, *cva;
   const int *gAssign;
   double *eps, *eps2, *eps_start, *deps, *beta, *xsq, *lambda, *hsv, *sigmaGG, *pi, *alpha;

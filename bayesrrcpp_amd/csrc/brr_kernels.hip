@@ -60,6 +60,47 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __hiloint2double(hi, lo);
 }
 
+// ------------------------------------------------------------------------------------
+// Genotype storage: f32 X, or 2-bit codes + a 4-entry value table per column (brr_device.hpp).
+// x_selk picks the value of the code in bits 2k, 2k+1 of b: two sign-extended bit extracts give
+// all-ones / all-zero masks and three bitfield inserts select (v_bfe_i32 + v_bfi_b32: no compare,
+// no VCC dependency, so the values of a byte decode in parallel).
+// (inline asm: written in C the compiler turns the masks back into compares and VCC selects)
+__device__ __forceinline__ uint32_t bfe_i1(uint32_t b, int pos) {
+  uint32_t m;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(b), "v"(pos));
+  return m;
+}
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {  // (m & a) | (~m & b)
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float x_selk(float4 l, uint32_t b, int k) {
+  const uint32_t m0 = bfe_i1(b, 2 * k), m1 = bfe_i1(b, 2 * k + 1);
+  const uint32_t lo = bfi(m0, __float_as_uint(l.y), __float_as_uint(l.x));
+  const uint32_t hi = bfi(m0, __float_as_uint(l.w), __float_as_uint(l.z));
+  return __uint_as_float(bfi(m1, hi, lo));
+}
+__device__ __forceinline__ float x_sel(float4 l, uint32_t c) { return x_selk(l, c, 0); }
+// rows 4k .. 4k+3 of a column from their code byte
+__device__ __forceinline__ float4 x_decode4(uint32_t b, float4 l) {
+  return make_float4(x_selk(l, b, 0), x_selk(l, b, 1), x_selk(l, b, 2), x_selk(l, b, 3));
+}
+__device__ __forceinline__ float4 x_lut(const Dev &d, int64_t col) {
+  return *reinterpret_cast<const float4 *>(d.xlut + 4 * col);
+}
+// one value (scattered reads: change lists, synthetic Y)
+__device__ __forceinline__ float x_at(const Dev &d, int64_t col, int64_t row) {
+  if (d.Xc) return x_sel(x_lut(d, col), (uint32_t)d.Xc[col * d.ldc + (row >> 2)] >> (2 * (row & 3)));
+  return d.X[col * d.ld + row];
+}
+// four consecutive rows row4 .. row4+3 (row4 a multiple of 4)
+__device__ __forceinline__ float4 x_at4(const Dev &d, int64_t col, int64_t row4) {
+  if (d.Xc) return x_decode4(d.Xc[col * d.ldc + (row4 >> 2)], x_lut(d, col));
+  return *reinterpret_cast<const float4 *>(d.X + col * d.ld + row4);
+}
+
 // Last-arriver ticket (cdna_hip_programming.md section 5, in-launch split-K reduction):
 // payload stores -> vmcnt(0) -> barrier -> release(agent) -> vmcnt(0) -> relaxed agent add;
 // the last arriver acquires (agent) before reading the other workgroups' payload.
@@ -173,8 +214,9 @@ __device__ __forceinline__ int genotype(uint64_t ds, int64_t i, int64_t j, uint3
   return u < t0 ? 0 : (u < t1 ? 1 : 2);
 }
 
-__global__ __launch_bounds__(256) void k_synth_x(float *X, int64_t ld, int64_t N, int64_t col0,
-                                                 uint64_t ds) {
+// f32 storage (X) or 2-bit codes (Xc, code = genotype, 3 = padding) + value table (xlut).
+__global__ __launch_bounds__(256) void k_synth_x(float *X, uint8_t *Xc, float *xlut, int64_t ld, int64_t ldc,
+                                                 int64_t N, int64_t col0, uint64_t ds) {
 #pragma clang fp contract(off)
   __shared__ double red[8];
   __shared__ int s_att;
@@ -183,7 +225,7 @@ __global__ __launch_bounds__(256) void k_synth_x(float *X, int64_t ld, int64_t N
   const double f = 0.05 + 0.45 * uniform(ds, T_DATA_FREQ, (uint32_t)j, 0, 0);
   const double t0 = (1.0 - f) * (1.0 - f);
   const double t1 = 1.0 - f * f;
-  float *x = X + jl * ld;
+  float *x = X ? X + jl * ld : nullptr;
   uint32_t att = 0;
   double S = 0.0, Q = 0.0;
   for (; att < 16; ++att) {
@@ -199,13 +241,33 @@ __global__ __launch_bounds__(256) void k_synth_x(float *X, int64_t ld, int64_t N
   }
   if (threadIdx.x == 0) s_att = (int)att;
   __syncthreads();
-  if (s_att == 16 || N < 2) {
-    for (int64_t i = threadIdx.x; i < ld; i += 256) x[i] = 0.f;
-    return;
-  }
+  const bool mono = s_att == 16 || N < 2;
   const double mean = S / (double)N;
   const double var = (Q - S * S / (double)N) / (double)(N - 1);
   const double sd = sqrt(var);
+  if (Xc) {
+    // value of genotype g = f32((g - mean) / sd), exactly the f32 storage's value
+    if (threadIdx.x < 4) {
+      const int g = threadIdx.x;
+      xlut[4 * jl + g] = (mono || g == 3) ? 0.f : (float)(((double)g - mean) / sd);
+    }
+    uint8_t *xc = Xc + jl * ldc;
+    for (int64_t b = threadIdx.x; b < ldc; b += 256) {
+      uint32_t byte = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t i = 4 * b + k;
+        const uint32_t c = (mono || i >= N) ? 3u : (uint32_t)genotype(ds, i, j, att, t0, t1);
+        byte |= c << (2 * k);
+      }
+      xc[b] = (uint8_t)byte;
+    }
+    return;
+  }
+  if (mono) {
+    for (int64_t i = threadIdx.x; i < ld; i += 256) x[i] = 0.f;
+    return;
+  }
   for (int64_t i = threadIdx.x; i < ld; i += 256) {
     float v = 0.f;
     if (i < N) v = (float)(((double)genotype(ds, i, j, att, t0, t1) - mean) / sd);
@@ -214,13 +276,12 @@ __global__ __launch_bounds__(256) void k_synth_x(float *X, int64_t ld, int64_t N
 }
 
 // y_i = sum_{causal j} x_ij beta_j  (causal list from the host)
-__global__ __launch_bounds__(256) void k_synth_y(const float *X, int64_t ld, int64_t N,
-                                                 const int *cidx, const double *cbeta, int nc,
+__global__ __launch_bounds__(256) void k_synth_y(Dev d, const int *cidx, const double *cbeta, int nc,
                                                  double *y) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= N) return;
+  if (i >= d.N) return;
   double acc = 0.0;
-  for (int c = 0; c < nc; ++c) acc += (double)X[(int64_t)cidx[c] * ld + i] * cbeta[c];
+  for (int c = 0; c < nc; ++c) acc += (double)x_at(d, cidx[c], i) * cbeta[c];
   y[i] = acc;
 }
 
@@ -244,8 +305,10 @@ __global__ void k_copy_f32(const float *src, int64_t lds, float *dst, int64_t ld
 // of cycle neighbours (also stored transposed in GT when GT != nullptr).  64x64 output tile per
 // workgroup, 4x4 per thread, 64-row chunks staged in LDS.  Element (i,j) and (j,i) of a
 // diagonal block accumulate identical products in identical order -> exactly symmetric.
-__global__ __launch_bounds__(256) void k_gram(const float *X, int64_t ld, const int *member,
-                                              const int *bsz, int B, int nb, int shift, double *G, double *GT) {
+__global__ __launch_bounds__(256) void k_gram(Dev d, const int *member, const int *bsz, int B, int nb, int shift,
+                                              double *G, double *GT) {
+  const float *X = d.X;
+  const int64_t ld = d.ld;
   __shared__ float As[64][65];
   __shared__ float Bs[64][65];
   const int gb = blockIdx.x;
@@ -263,13 +326,23 @@ __global__ __launch_bounds__(256) void k_gram(const float *X, int64_t ld, const 
   // loader: column c = t >> 2 (0..63), rows (t & 3) * 16 .. +16
   const int lc = t >> 2, lr = (t & 3) * 16;
   const int ci = ti * 64 + lc, cj = tj * 64 + lc;
-  const float *pa = (ci < bs) ? X + (int64_t)member[(int64_t)gb * B + ci] * ld : nullptr;
-  const float *pb = (cj < bs2) ? X + (int64_t)member[(int64_t)gb2 * B + cj] * ld : nullptr;
+  const int64_t ca = (ci < bs) ? member[(int64_t)gb * B + ci] : -1;
+  const int64_t cb = (cj < bs2) ? member[(int64_t)gb2 * B + cj] : -1;
+  const float *pa = (ca >= 0 && X) ? X + ca * ld : nullptr;
+  const float *pb = (cb >= 0 && X) ? X + cb * ld : nullptr;
+  const float4 z4 = make_float4(0, 0, 0, 0);
+  const float4 la = (ca >= 0 && d.Xc) ? x_lut(d, ca) : z4, lb = (cb >= 0 && d.Xc) ? x_lut(d, cb) : z4;
   for (int64_t r0 = 0; r0 < ld; r0 += 64) {
 #pragma unroll
     for (int q = 0; q < 16; q += 4) {
-      float4 va = pa ? *reinterpret_cast<const float4 *>(pa + r0 + lr + q) : make_float4(0, 0, 0, 0);
-      float4 vb = pb ? *reinterpret_cast<const float4 *>(pb + r0 + lr + q) : make_float4(0, 0, 0, 0);
+      float4 va, vb;
+      if (d.Xc) {  // 2-bit codes: the same f32 values, decoded
+        va = ca >= 0 ? x_decode4(d.Xc[ca * d.ldc + ((r0 + lr + q) >> 2)], la) : z4;
+        vb = cb >= 0 ? x_decode4(d.Xc[cb * d.ldc + ((r0 + lr + q) >> 2)], lb) : z4;
+      } else {
+        va = pa ? *reinterpret_cast<const float4 *>(pa + r0 + lr + q) : z4;
+        vb = pb ? *reinterpret_cast<const float4 *>(pb + r0 + lr + q) : z4;
+      }
       As[lr + q + 0][lc] = va.x; As[lr + q + 1][lc] = va.y; As[lr + q + 2][lc] = va.z; As[lr + q + 3][lc] = va.w;
       Bs[lr + q + 0][lc] = vb.x; Bs[lr + q + 1][lc] = vb.y; Bs[lr + q + 2][lc] = vb.z; Bs[lr + q + 3][lc] = vb.w;
     }
@@ -334,7 +407,7 @@ __global__ __launch_bounds__(256) void k_rows(Dev d, int flags, const double *de
   if (flags & ROW_PENDING) {
     // the last one or two blocks' changes (slots slot_a then slot_b; -1 = none), lists padded
     // to a multiple of 16 with neutral entries
-    const float *Xr = d.X + (valid ? row : 0);
+    const int64_t rowc = valid ? row : 0;
     for (int k = 0; k < 2; ++k) {
       const int slot = k == 0 ? slot_a : slot_b;
       if (slot < 0) continue;
@@ -344,7 +417,7 @@ __global__ __launch_bounds__(256) void k_rows(Dev d, int flags, const double *de
       for (int p0 = 0; p0 < np; p0 += 8) {
         double x[8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) x[q] = (double)Xr[(int64_t)pidx[p0 + q] * d.ld];
+        for (int q = 0; q < 8; ++q) x[q] = (double)x_at(d, pidx[p0 + q], rowc);
 #pragma unroll
         for (int q = 0; q < 8; ++q) e = (e + x[q] * pbo[p0 + q]) - x[q] * pbn[p0 + q];
       }
@@ -811,14 +884,17 @@ __global__ __launch_bounds__(256, 2) void k_stream(Dev d, int s, const double *e
   const int64_t row0 = (int64_t)rg * SROWS + 4 * lane;
   const bool valid = row0 < d.N;
   const int64_t rowc = valid ? row0 : 0;
-  const float *Xr = d.X + rowc;
-  const int64_t ld = d.ld;
   const int par = s & 1;
   // block columns first: their loads depend on nothing
   const int *mem = d.member + (int64_t)s * B + cc * CB + w * CW;
   float4 x[CW];
+  if (d.Xc) {
 #pragma unroll
-  for (int j = 0; j < CW; ++j) x[j] = *reinterpret_cast<const float4 *>(Xr + (int64_t)mem[j] * ld);
+    for (int j = 0; j < CW; ++j) x[j] = x_at4(d, mem[j], rowc);
+  } else {
+#pragma unroll
+    for (int j = 0; j < CW; ++j) x[j] = *reinterpret_cast<const float4 *>(d.X + rowc + (int64_t)mem[j] * d.ld);
+  }
   const double2 ea = *reinterpret_cast<const double2 *>(eps_in + rowc);
   const double2 eb = *reinterpret_cast<const double2 *>(eps_in + rowc + 2);
   double e0 = ea.x, e1 = ea.y, e2 = eb.x, e3 = eb.y;
@@ -846,7 +922,9 @@ __global__ __launch_bounds__(256, 2) void k_stream(Dev d, int s, const double *e
     for (int p0 = 0; p0 < np; p0 += 16) {
       float4 xp[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) xp[q] = *reinterpret_cast<const float4 *>(Xr + (int64_t)s_pidx[p0 + q] * ld);
+      for (int q = 0; q < 16; ++q)
+        xp[q] = d.Xc ? x_at4(d, s_pidx[p0 + q], rowc)
+                     : *reinterpret_cast<const float4 *>(d.X + rowc + (int64_t)s_pidx[p0 + q] * d.ld);
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const double bo = s_pbo[p0 + q], bn = s_pbn[p0 + q];
@@ -1820,12 +1898,16 @@ constexpr int SWEEP_NW = SWEEP_NT / 64;
 #ifndef STREAM_P
 #define STREAM_P 1    // items in flight ahead of the one being consumed (2+ spills at CW = 16)
 #endif
+#ifndef STREAM_P2
+#define STREAM_P2 3   // the same for 2-bit codes (a byte per column and lane; vmcnt <= 63 caps P CW)
+#endif
 constexpr int FUSED_GROUP = 16;  // streaming workgroups (slab rows) per level-2 reduction group
 
 // Block `slot`'s change list applied to this workgroup's residual rows:
 // eps_i += x_ij b_old - x_ij b_new in list order (BayesRv2.cpp:191,243).  The rows are cut into
 // 64-row slices, one row per lane, spread over the 8 waves; each wave keeps two batches of 16
 // column loads in flight (the list is padded to a multiple of 16 with neutral entries).
+template <int XF>
 __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0, int64_t r1, int npass,
                                               double *eps_l, int *s_pidx, double *s_pbo, double *s_pbn,
                                               int *s_np) {
@@ -1850,18 +1932,23 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
   for (int sl = w; sl < npass * 4; sl += SWEEP_NW) {
     const int off = sl * 64 + lane;
     const bool ok = r0 + off < r1;  // rows beyond r1 read row r0 (unconditional loads) and are not stored
-    const float *Xr = d.X + (ok ? r0 + off : r0);
+    const int64_t rr = ok ? r0 + off : r0;
+    const float *Xr = XF ? nullptr : d.X + rr;
+    auto xload = [&](int col) __attribute__((always_inline)) -> float {
+      if constexpr (XF) return x_at(d, col, rr);
+      else return Xr[(int64_t)col * ld];
+    };
     double e = eps_l[off];
     float xa[AB], xb[AB];
     if (np > 0) {
 #pragma unroll
-      for (int q = 0; q < AB; ++q) xa[q] = Xr[(int64_t)s_pidx[q] * ld];
+      for (int q = 0; q < AB; ++q) xa[q] = xload(s_pidx[q]);
     }
     for (int p0 = 0; p0 < np; p0 += 2 * AB) {
       const bool more = p0 + AB < np;
       if (more) {
 #pragma unroll
-        for (int q = 0; q < AB; ++q) xb[q] = Xr[(int64_t)s_pidx[p0 + AB + q] * ld];
+        for (int q = 0; q < AB; ++q) xb[q] = xload(s_pidx[p0 + AB + q]);
       }
 #pragma unroll
       for (int q = 0; q < AB; ++q) {
@@ -1871,7 +1958,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
       if (!more) break;
       if (p0 + 2 * AB < np) {
 #pragma unroll
-        for (int q = 0; q < AB; ++q) xa[q] = Xr[(int64_t)s_pidx[p0 + 2 * AB + q] * ld];
+        for (int q = 0; q < AB; ++q) xa[q] = xload(s_pidx[p0 + 2 * AB + q]);
       }
 #pragma unroll
       for (int q = 0; q < AB; ++q) {
@@ -1884,9 +1971,13 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
   __syncthreads();
 }
 
-template <int CW, int P>
+// XF = 1: 2-bit genotype codes.  The ring then holds one code byte (4 rows) per column and lane,
+// and the value tables of the block being consumed are staged in LDS (s_lut, B entries) at each
+// block boundary, after the previous block's last item and before the barrier that precedes the
+// first item of the block.
+template <int CW, int P, int XF>
 __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int npass, double *eps_l, int *s_pidx,
-                                            double *s_pbo, double *s_pbn, int *s_np) {
+                                            double *s_pbo, double *s_pbn, int *s_np, float4 *s_lut) {
 #pragma clang fp contract(off)
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -1894,7 +1985,13 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   const int B = d.B, nb = d.nb;
   const int64_t ld = d.ld;
   const bool prof = d.sc->prof_on;
+  auto stage_lut = [&](int s) __attribute__((always_inline)) {
+    if constexpr (XF) {
+      for (int i = t; i < B; i += SWEEP_NT) s_lut[i] = x_lut(d, d.member[(int64_t)s * B + i]);
+    }
+  };
   for (int i = t; i < npass * SROWS; i += SWEEP_NT) eps_l[i] = r0 + i < r1 ? d.eps[r0 + i] : 0.0;
+  stage_lut(0);
   __syncthreads();
   const int CPW = B / SWEEP_NW;  // columns per wave
   const int NCH = CPW / CW;      // chunks per wave and block
@@ -1905,17 +2002,24 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   // residual rows are 0, so they add exactly 0); rows in [N, ld) are zero padding of X.  The
   // loads stay unconditional: a divergent branch here would turn the wave-uniform member
   // loads into vector loads whose wait drains the prefetch ring.
-  auto issue = [&](int it, float4 (&x)[CW]) {
+  using Raw = typename std::conditional<XF != 0, uint32_t, float4>::type;
+  auto issue = [&](int it, Raw (&x)[CW]) {
     const int s = it / items, rem = it - s * items;
     const int c = rem / npass, p = rem - c * npass;
     const int64_t off = r0 + p * SROWS + 4 * lane < r1 ? r0 + p * SROWS + 4 * lane : r0;
-    const float *base = d.X + off;
     const int *mem = d.member + (int64_t)s * B + w * CPW + c * CW;  // wave-uniform: scalar loads
+    if constexpr (XF) {
+      const uint8_t *base = d.Xc + (off >> 2);
 #pragma unroll
-    for (int j = 0; j < CW; ++j) x[j] = ldg4(base + (int64_t)mem[j] * ld);
+      for (int j = 0; j < CW; ++j) x[j] = base[(int64_t)mem[j] * d.ldc];
+    } else {
+      const float *base = d.X + off;
+#pragma unroll
+      for (int j = 0; j < CW; ++j) x[j] = ldg4(base + (int64_t)mem[j] * ld);
+    }
   };
   // register ring of P + 1 items: item it + P is issued before item it is consumed
-  float4 xq[P + 1][CW];
+  Raw xq[P + 1][CW];
   double v[CW];
 #pragma unroll
   for (int j = 0; j < CW; ++j) v[j] = 0.0;
@@ -1928,8 +2032,14 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     const int s = it / items, rem = it - s * items;
     const int c = rem / npass, p = rem - c * npass;
     const bool blk_end = rem == items - 1;
+    if (XF && rem == 0 && s == 1) {  // (every wave passed block 0's closing barrier)
+      stage_lut(1);
+      __syncthreads();
+    }
     if (rem == 0 && s >= 2) {
-      // block boundary: bring the residual rows from E_{s-2} to E_{s-1} (block s-2's changes)
+      // block boundary: bring the residual rows from E_{s-2} to E_{s-1} (block s-2's changes);
+      // the value tables of block s go to LDS before apply_pending's first barrier
+      stage_lut(s);
       if (t == 0) {
         wait_geq(d.sync + SY_PEND, d.sbase + s - 1, d.sync, 2);
         if (prof) {
@@ -1940,7 +2050,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
           t_mark = tn;
         }
       }
-      apply_pending(d, (s - 2) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np);
+      apply_pending<XF>(d, (s - 2) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np);
       if (prof && t == 0) {
         tr_last(d, s, TR_APPLY_LAST);
         if (s == nb / 2) d.trace[(int64_t)nb * 16 + 1024 + g] = wall_clock64();  // per-workgroup probe
@@ -1955,8 +2065,12 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     const double *e = eps_l + p * SROWS + 4 * lane;
     const double e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
 #pragma unroll
-    for (int j = 0; j < CW; ++j)
-      v[j] += (((double)xq[0][j].x * e0 + (double)xq[0][j].y * e1) + (double)xq[0][j].z * e2) + (double)xq[0][j].w * e3;
+    for (int j = 0; j < CW; ++j) {
+      float4 xv;
+      if constexpr (XF) xv = x_decode4(xq[0][j], s_lut[w * CPW + c * CW + j]);
+      else xv = xq[0][j];
+      v[j] += (((double)xv.x * e0 + (double)xv.y * e1) + (double)xv.z * e2) + (double)xv.w * e3;
+    }
 #pragma unroll
     for (int q = 0; q < P; ++q)
 #pragma unroll
@@ -2008,9 +2122,9 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   }
   // end of sweep: the last two blocks' changes, then the residual rows back to HBM
   if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + nb, d.sync, 4);
-  if (nb >= 2) apply_pending(d, (nb - 2) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np);
+  if (nb >= 2) apply_pending<XF>(d, (nb - 2) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np);
   else __syncthreads();
-  apply_pending(d, (nb - 1) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np);
+  apply_pending<XF>(d, (nb - 1) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np);
   for (int i = t; i < npass * SROWS; i += SWEEP_NT)
     if (r0 + i < r1) d.eps[r0 + i] = eps_l[i];
 }
@@ -2054,7 +2168,7 @@ __device__ __forceinline__ void solver_role(const Dev &d, uint32_t it, int nslot
   }
 }
 
-template <bool HS, int B>
+template <bool HS, int B, int XF>
 __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int nslot, int nsg, int rpw, int npass,
                                                         int nred) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2070,11 +2184,15 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
   } else if ((int)blockIdx.x > nsg) {
     reduce_role(d, (int)blockIdx.x - 1 - nsg, nsg, nred, d.sc->prof_on);
   } else {
-    // streamer LDS: residual rows, then the change list being applied (stream_lds_bytes)
+    // streamer LDS: residual rows, [value tables of the block (2-bit codes)], the change list
+    // being applied (fused_config)
     double *eps_l = reinterpret_cast<double *>(smem);
-    double *s_pbo = eps_l + (int64_t)npass * SROWS, *s_pbn = s_pbo + (d.B + 16);
+    float4 *s_lut = reinterpret_cast<float4 *>(eps_l + (int64_t)npass * SROWS);
+    double *s_pbo = reinterpret_cast<double *>(s_lut + (XF ? d.B : 0)), *s_pbn = s_pbo + (d.B + 16);
     int *s_pidx = reinterpret_cast<int *>(s_pbn + (d.B + 16));
-    stream_role<STREAM_CW, STREAM_P>(d, (int)blockIdx.x - 1, rpw, npass, eps_l, s_pidx, s_pbo, s_pbn, &s_np);
+    stream_role<STREAM_CW, XF ? STREAM_P2 : STREAM_P, XF>(d, (int)blockIdx.x - 1, rpw, npass, eps_l, s_pidx, s_pbo,
+                                                         s_pbn, &s_np,
+                                         s_lut);
   }
 }
 
@@ -2261,15 +2379,14 @@ namespace brr {
 
 static inline unsigned cdiv64(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
 
-hipError_t launch_synth_x(float *X, int64_t ld, int64_t N, int64_t M, int64_t col0, uint64_t ds,
-                          hipStream_t st) {
-  hipLaunchKernelGGL(k_synth_x, dim3((unsigned)M), dim3(256), 0, st, X, ld, N, col0, ds);
+hipError_t launch_synth_x(const Dev &d, uint64_t ds, hipStream_t st) {
+  hipLaunchKernelGGL(k_synth_x, dim3((unsigned)d.M), dim3(256), 0, st, const_cast<float *>(d.X),
+                     const_cast<uint8_t *>(d.Xc), const_cast<float *>(d.xlut), d.ld, d.ldc, d.N, d.col_offset, ds);
   return hipGetLastError();
 }
 
-hipError_t launch_synth_y(const float *X, int64_t ld, int64_t N, const int *cidx, const double *cb,
-                          int nc, double *y, hipStream_t st) {
-  hipLaunchKernelGGL(k_synth_y, dim3(cdiv64(N, 256)), dim3(256), 0, st, X, ld, N, cidx, cb, nc, y);
+hipError_t launch_synth_y(const Dev &d, const int *cidx, const double *cb, int nc, double *y, hipStream_t st) {
+  hipLaunchKernelGGL(k_synth_y, dim3(cdiv64(d.N, 256)), dim3(256), 0, st, d, cidx, cb, nc, y);
   return hipGetLastError();
 }
 
@@ -2285,8 +2402,8 @@ hipError_t launch_cast_x(const void *src, bool is_f64, int64_t lds, float *dst, 
 
 hipError_t launch_gram(const Dev &d, int shift, double *G, double *GT, hipStream_t st) {
   const int nt = (d.B + 63) / 64;
-  hipLaunchKernelGGL(k_gram, dim3((unsigned)d.nb, (unsigned)(nt * nt)), dim3(256), 0, st, d.X, d.ld, d.member,
-                     d.bsz, d.B, d.nb, shift, G, GT);
+  hipLaunchKernelGGL(k_gram, dim3((unsigned)d.nb, (unsigned)(nt * nt)), dim3(256), 0, st, d, d.member, d.bsz, d.B,
+                     d.nb, shift, G, GT);
   return hipGetLastError();
 }
 
@@ -2341,16 +2458,19 @@ hipError_t launch_stream(const Dev &d, int s, const double *eps_in, double *eps_
 // Fused sweep geometry: one solver, nsg streaming and nred reducing workgroups, one per CU (the
 // solver's LDS), each streamer owning rpw rows (npass passes of 256).  Returns false when the
 // configuration cannot be made resident (the per-block kernels are used then).
+// (B = 64 never fuses: a block must give every wave whole STREAM_CW-column chunks)
 template <bool HS, int B>
-static const void *sweep_fn() { return (const void *)k_sweep<HS, B>; }
+static const void *sweep_fn(bool xf) {
+  return xf ? (const void *)k_sweep<HS, B, 1> : (const void *)k_sweep<HS, B, 0>;
+}
 
-static const void *sweep_kernel(int model, int B) {
+static const void *sweep_kernel(int model, int B, bool xf) {
   const bool hs = model == MODEL_HORSESHOE;
   switch (B) {
-    case 64: return hs ? sweep_fn<true, 64>() : sweep_fn<false, 64>();
-    case 128: return hs ? sweep_fn<true, 128>() : sweep_fn<false, 128>();
-    case 256: return hs ? sweep_fn<true, 256>() : sweep_fn<false, 256>();
-    default: return hs ? sweep_fn<true, 512>() : sweep_fn<false, 512>();
+    case 128: return hs ? sweep_fn<true, 128>(xf) : sweep_fn<false, 128>(xf);
+    case 256: return hs ? sweep_fn<true, 256>(xf) : sweep_fn<false, 256>(xf);
+    case 512: return hs ? sweep_fn<true, 512>(xf) : sweep_fn<false, 512>(xf);
+    default: return nullptr;
   }
 }
 
@@ -2374,7 +2494,9 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   const int npass = (int)((rpw + SROWS - 1) / SROWS);
   const int nred = ngr(nsg);
   if (nsg > d.RG + 1) return false;  // slab1 rows
-  const void *fn = sweep_kernel(d.model, d.B);
+  const bool xf = d.Xc != nullptr;
+  const void *fn = sweep_kernel(d.model, d.B, xf);
+  if (!fn) return false;
   hipFuncAttributes attr;
   if (hipFuncGetAttributes(&attr, fn) != hipSuccess) return false;
   const size_t budget = SOLVE_LDS_MAX - attr.sharedSizeBytes;
@@ -2383,8 +2505,10 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   if (fixed + 8 * (size_t)d.B > budget) return false;
   const int nslot = (int)std::min<size_t>((size_t)solve_max_slots(d.B, SWEEP_NT), (budget - fixed) / (8 * (size_t)d.B));
   if ((size_t)nslot * d.B < solve_scratch_doubles(d.B, SWEEP_NT)) return false;
-  // streamers: residual rows + the change list (indices, old and new betas) in LDS
-  const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double) + (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int));
+  // streamers: residual rows, [the block's value tables], the change list (indices, old and new
+  // betas) in LDS
+  const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double) + (xf ? (size_t)d.B * 16 : 0) +
+                           (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int));
   const size_t lds = std::max(fixed + (size_t)nslot * 8 * d.B, eps_bytes);
   if (lds > budget) return false;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) != hipSuccess) return false;
@@ -2402,15 +2526,20 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
 }
 
 hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipStream_t st) {
-  const bool hs = d.model == MODEL_HORSESHOE;
+  const bool hs = d.model == MODEL_HORSESHOE, xf = d.Xc != nullptr;
   const dim3 grid((unsigned)(c.nsg + 1 + c.nred)), blk(SWEEP_NT);
-#define BRR_SWEEP_LAUNCH(HSV, BV) \
-  hipLaunchKernelGGL((k_sweep<HSV, BV>), grid, blk, c.lds, st, d, it, c.nslot, c.nsg, c.rpw, c.npass, c.nred)
+#define BRR_SWEEP_LAUNCH(HSV, BV)                                                                                  \
+  do {                                                                                                             \
+    if (xf) hipLaunchKernelGGL((k_sweep<HSV, BV, 1>), grid, blk, c.lds, st, d, it, c.nslot, c.nsg, c.rpw, c.npass, \
+                               c.nred);                                                                            \
+    else hipLaunchKernelGGL((k_sweep<HSV, BV, 0>), grid, blk, c.lds, st, d, it, c.nslot, c.nsg, c.rpw, c.npass,    \
+                            c.nred);                                                                               \
+  } while (0)
   switch (d.B) {
-    case 64: if (hs) BRR_SWEEP_LAUNCH(true, 64); else BRR_SWEEP_LAUNCH(false, 64); break;
     case 128: if (hs) BRR_SWEEP_LAUNCH(true, 128); else BRR_SWEEP_LAUNCH(false, 128); break;
     case 256: if (hs) BRR_SWEEP_LAUNCH(true, 256); else BRR_SWEEP_LAUNCH(false, 256); break;
-    default: if (hs) BRR_SWEEP_LAUNCH(true, 512); else BRR_SWEEP_LAUNCH(false, 512); break;
+    case 512: if (hs) BRR_SWEEP_LAUNCH(true, 512); else BRR_SWEEP_LAUNCH(false, 512); break;
+    default: return hipErrorInvalidValue;
   }
 #undef BRR_SWEEP_LAUNCH
   return hipGetLastError();

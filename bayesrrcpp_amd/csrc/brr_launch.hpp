@@ -12,10 +12,8 @@ enum RowFlagsHost : int {
 };
 enum MarkerModeHost : int { H_MR_BAYESR = 0, H_MR_HS = 1, H_MR_COUNT_ALL = 2 };
 
-hipError_t launch_synth_x(float *X, int64_t ld, int64_t N, int64_t M, int64_t col0, uint64_t ds,
-                          hipStream_t st);
-hipError_t launch_synth_y(const float *X, int64_t ld, int64_t N, const int *cidx, const double *cb,
-                          int nc, double *y, hipStream_t st);
+hipError_t launch_synth_x(const Dev &d, uint64_t ds, hipStream_t st);
+hipError_t launch_synth_y(const Dev &d, const int *cidx, const double *cb, int nc, double *y, hipStream_t st);
 hipError_t launch_cast_x(const void *src, bool is_f64, int64_t lds, float *dst, int64_t ldd,
                          int64_t N, int64_t M, hipStream_t st);
 hipError_t launch_gram(const Dev &d, int shift, double *G, double *GT, hipStream_t st);

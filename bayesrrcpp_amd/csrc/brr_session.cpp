@@ -129,6 +129,7 @@ struct brr_session {
   int shard = 0, nshard = 1;
   int32_t iteration = 0;
   bool initialized = false, pi_given = false, need_reduce = false, have_y = false, have_x = false;
+  bool x2bit = false;  // genotype storage: 2-bit codes (opt.x_storage == BRR_X_2BIT)
   double mu0 = 0, sigmaE0 = 0;
   double *ex_eps = nullptr, *ex_stats = nullptr;  // exchange buffers (caller- or session-owned)
   bool ex_owned = false;
@@ -478,7 +479,15 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   d.MRG = (int)((M + 255) / 256);
   const int64_t RGrows = (N + 255) / 256;
   int rc = 0;
-  rc |= s->alloc(const_cast<float **>(&d.X), d.ld * M);
+  // genotype storage: f32 (default) or 2-bit codes + per-column value tables
+  s->x2bit = opt.x_storage == BRR_X_2BIT;
+  d.ldc = d.ld / 4;
+  if (s->x2bit) {
+    rc |= s->alloc(const_cast<uint8_t **>(&d.Xc), d.ldc * M);
+    rc |= s->alloc(const_cast<float **>(&d.xlut), 4 * M);
+  } else {
+    rc |= s->alloc(const_cast<float **>(&d.X), d.ld * M);
+  }
   rc |= s->alloc(const_cast<double **>(&d.Y), N);
   rc |= s->alloc(const_cast<double **>(&d.fixed), N * std::max<int64_t>(F, 1));
   rc |= s->alloc(const_cast<double **>(&d.cva), (int64_t)groups * std::max(K - 1, 1));
@@ -545,7 +554,9 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
             hipMemsetAsync(d.mcnt, 0, sizeof(int), s->st) == hipSuccess &&
             hipMemsetAsync(d.sc, 0, sizeof(Scal), s->st) == hipSuccess &&
             hipMemsetAsync(d.stats, 0, sizeof(double) * s->NS, s->st) == hipSuccess &&
-            hipMemsetAsync(const_cast<float *>(d.X), 0, sizeof(float) * d.ld * M, s->st) == hipSuccess &&
+            (s->x2bit ? hipMemsetAsync(const_cast<uint8_t *>(d.Xc), 0xFF, (size_t)d.ldc * M, s->st) == hipSuccess &&
+                            hipMemsetAsync(const_cast<float *>(d.xlut), 0, sizeof(float) * 4 * M, s->st) == hipSuccess
+                      : hipMemsetAsync(const_cast<float *>(d.X), 0, sizeof(float) * d.ld * M, s->st) == hipSuccess) &&
             hipMemsetAsync(d.alpha, 0, sizeof(double) * std::max<int64_t>(F, 1), s->st) == hipSuccess &&
             hipMemsetAsync(const_cast<double *>(d.fixed), 0, sizeof(double) * N * std::max<int64_t>(F, 1), s->st) == hipSuccess &&
             set_solve_lds_limit(B) == hipSuccess && hipStreamSynchronize(s->st) == hipSuccess;
@@ -574,10 +585,109 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
 
 void brr_session_destroy(brr_session *s) { delete s; }
 
+// 2-bit encoding of columns c0 .. c0+nc-1 of a host matrix (f64 or f32, leading dimension ldx):
+// each column's distinct f32 values plus 0 (the padding rows) must number at most 4; codes are
+// their ranks in ascending order (bit pattern order), so the device decodes exactly the f32
+// values the f32 storage would hold.  Threads split the columns.  Returns the first offending
+// column, or -1.
+static int64_t encode_2bit(const void *X, bool f64, int64_t ldx, int64_t N, int64_t ldc, int64_t c0, int64_t nc,
+                           uint8_t *codes, float *lut) {
+  std::atomic<int64_t> bad{-1};
+  auto work = [&](int64_t a, int64_t b) {
+    for (int64_t j = a; j < b && bad.load() < 0; ++j) {
+      const int64_t col = c0 + j;
+      auto val = [&](int64_t i) -> float {
+        return f64 ? (float)((const double *)X)[ldx * col + i] : ((const float *)X)[ldx * col + i];
+      };
+      uint32_t vals[4];
+      int nv = 0;
+      auto add = [&](uint32_t u) -> bool {
+        for (int k = 0; k < nv; ++k)
+          if (vals[k] == u) return true;
+        if (nv == 4) return false;
+        vals[nv++] = u;
+        return true;
+      };
+      bool ok = add(0u);  // +0.0f: padding rows
+      for (int64_t i = 0; i < N && ok; ++i) {
+        const float v = val(i);
+        uint32_t u;
+        std::memcpy(&u, &v, 4);
+        ok = add(u);
+      }
+      if (!ok) {
+        int64_t exp = -1;
+        bad.compare_exchange_strong(exp, col);
+        return;
+      }
+      float fv[4];
+      for (int k = 0; k < nv; ++k) std::memcpy(&fv[k], &vals[k], 4);
+      // ascending value order (ties impossible: distinct bit patterns; -0 < +0 by pattern)
+      std::sort(vals, vals + nv, [](uint32_t x, uint32_t y) {
+        float a, b;
+        std::memcpy(&a, &x, 4);
+        std::memcpy(&b, &y, 4);
+        return a < b || (a == b && x > y);
+      });
+      uint8_t zero_code = 0;
+      for (int k = 0; k < nv; ++k) {
+        std::memcpy(&lut[4 * j + k], &vals[k], 4);
+        if (vals[k] == 0u) zero_code = (uint8_t)k;
+      }
+      for (int k = nv; k < 4; ++k) lut[4 * j + k] = 0.f;
+      (void)fv;
+      uint8_t *cc = codes + j * ldc;
+      for (int64_t b4 = 0; b4 < ldc; ++b4) {
+        uint32_t byte = 0;
+        for (int k = 0; k < 4; ++k) {
+          const int64_t i = 4 * b4 + k;
+          uint32_t code = zero_code;
+          if (i < N) {
+            const float v = val(i);
+            uint32_t u;
+            std::memcpy(&u, &v, 4);
+            for (int q = 0; q < nv; ++q)
+              if (vals[q] == u) code = (uint32_t)q;
+          }
+          byte |= code << (2 * k);
+        }
+        cc[b4] = (uint8_t)byte;
+      }
+    }
+  };
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::max(1u, std::thread::hardware_concurrency()),
+                                                             (int64_t)16, nc}));
+  std::vector<std::thread> pool;
+  for (int t = 0; t < nt; ++t) pool.emplace_back(work, nc * t / nt, nc * (t + 1) / nt);
+  for (auto &th : pool) th.join();
+  return bad.load();
+}
+
 static int upload_x_any(brr_session *s, const void *X, bool f64, int64_t ldx) {
   if (!s || !X) { set_error("null argument"); return -1; }
   if (ldx < s->N) { set_error("ldx < N"); return -1; }
   HIPCHK(hipSetDevice(s->device));
+  if (s->x2bit) {
+    const int64_t ldc = s->d.ldc;
+    const int64_t chunk_cols = std::max<int64_t>(1, std::min<int64_t>(s->M, (int64_t)(256ll << 20) / ldc));
+    std::vector<uint8_t> codes((size_t)(ldc * chunk_cols));
+    std::vector<float> lut((size_t)(4 * chunk_cols));
+    for (int64_t c0 = 0; c0 < s->M; c0 += chunk_cols) {
+      const int64_t nc = std::min<int64_t>(chunk_cols, s->M - c0);
+      const int64_t bad = encode_2bit(X, f64, ldx, s->N, ldc, c0, nc, codes.data(), lut.data());
+      if (bad >= 0) {
+        set_error("column %lld has more than 3 distinct non-zero values: 2-bit genotype storage needs "
+                  "genotype-coded columns (x_storage = BRR_X_F32 stores any matrix)", (long long)bad);
+        return -1;
+      }
+      HIPCHK(hipMemcpy(const_cast<uint8_t *>(s->d.Xc) + ldc * c0, codes.data(), (size_t)(ldc * nc),
+                       hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(const_cast<float *>(s->d.xlut) + 4 * c0, lut.data(), sizeof(float) * 4 * nc,
+                       hipMemcpyHostToDevice));
+    }
+    s->have_x = true;
+    return 0;
+  }
   const size_t esz = f64 ? 8 : 4;
   const int64_t chunk_cols = std::min<int64_t>(
       65535, std::max<int64_t>(1, (int64_t)(256ll << 20) / (int64_t)(esz * ldx)));  // grid.y limit
@@ -604,10 +714,67 @@ static int upload_x_any(brr_session *s, const void *X, bool f64, int64_t ldx) {
 int brr_session_upload_x_f64(brr_session *s, const double *X, int64_t ldx) { return upload_x_any(s, X, true, ldx); }
 int brr_session_upload_x_f32(brr_session *s, const float *X, int64_t ldx) { return upload_x_any(s, X, false, ldx); }
 
+// PLINK .bed body (SNP-major, after the 3 magic bytes): this shard's M columns of bytes_per_col
+// >= ceil(N/4) bytes, sample i in bits 2(i&3).. of byte i>>2; codes 00 = two copies of allele 1,
+// 10 = heterozygous, 11 = no copy, 01 = missing.  Genotype g = copies of allele 1; columns are
+// standardised as R's scale() after mean imputation (vignettes/BayesRR.Rmd:92): mean over the
+// observed samples, sd = sqrt(sum_observed (g - mean)^2 / (N - 1)), x = f32((g - mean) / sd), a
+// missing sample gets x = 0; a column without variation is all 0.
+int brr_session_upload_bed(brr_session *s, const uint8_t *bed, int64_t bytes_per_col) {
+  if (!s || !bed) { set_error("null argument"); return -1; }
+  const int64_t N = s->N, nbytes = (N + 3) / 4;
+  if (bytes_per_col < nbytes) { set_error("bytes_per_col < ceil(N/4)"); return -1; }
+  HIPCHK(hipSetDevice(s->device));
+  const int64_t ldc = s->d.ldc;
+  const int64_t chunk_cols = std::max<int64_t>(1, std::min<int64_t>(s->M, (int64_t)(256ll << 20) / ldc));
+  std::vector<uint8_t> codes;
+  std::vector<float> lut((size_t)(4 * chunk_cols)), xf;
+  if (s->x2bit) codes.resize((size_t)(ldc * chunk_cols));
+  else xf.resize((size_t)(s->d.ld * chunk_cols));
+  static const double gval[4] = {2.0, 0.0 /* missing */, 1.0, 0.0};
+  for (int64_t c0 = 0; c0 < s->M; c0 += chunk_cols) {
+    const int64_t nc = std::min<int64_t>(chunk_cols, s->M - c0);
+    for (int64_t j = 0; j < nc; ++j) {
+      const uint8_t *src = bed + bytes_per_col * (c0 + j);
+      int64_t cnt[4] = {0, 0, 0, 0};
+      for (int64_t i = 0; i < N; ++i) cnt[(src[i >> 2] >> (2 * (i & 3))) & 3]++;
+      const int64_t nobs = cnt[0] + cnt[2] + cnt[3];
+      const double S = 2.0 * cnt[0] + cnt[2], Q = 4.0 * cnt[0] + cnt[2];
+      const double mean = nobs > 0 ? S / (double)nobs : 0.0;
+      const double ss = Q - S * mean;  // sum over observed samples of (g - mean)^2
+      const bool flat = nobs < 2 || !(ss > 0.0) || N < 2;
+      const double sd = flat ? 1.0 : std::sqrt(ss / (double)(N - 1));
+      float *l = &lut[(size_t)(4 * j)];
+      for (int c = 0; c < 4; ++c) l[c] = (flat || c == 1) ? 0.f : (float)((gval[c] - mean) / sd);
+      if (s->x2bit) {
+        uint8_t *dst = &codes[(size_t)(ldc * j)];
+        std::memcpy(dst, src, (size_t)nbytes);
+        if (N & 3) dst[nbytes - 1] = (uint8_t)((dst[nbytes - 1] & ((1u << (2 * (N & 3))) - 1u)) |
+                                               (0x55u & ~((1u << (2 * (N & 3))) - 1u)));  // padding: code 01 -> 0
+        std::memset(dst + nbytes, 0x55, (size_t)(ldc - nbytes));
+      } else {
+        float *dst = &xf[(size_t)(s->d.ld * j)];
+        for (int64_t i = 0; i < s->d.ld; ++i) dst[i] = i < N ? l[(src[i >> 2] >> (2 * (i & 3))) & 3] : 0.f;
+      }
+    }
+    if (s->x2bit) {
+      HIPCHK(hipMemcpy(const_cast<uint8_t *>(s->d.Xc) + ldc * c0, codes.data(), (size_t)(ldc * nc),
+                       hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(const_cast<float *>(s->d.xlut) + 4 * c0, lut.data(), sizeof(float) * 4 * nc,
+                       hipMemcpyHostToDevice));
+    } else {
+      HIPCHK(hipMemcpy(const_cast<float *>(s->d.X) + s->d.ld * c0, xf.data(), sizeof(float) * s->d.ld * nc,
+                       hipMemcpyHostToDevice));
+    }
+  }
+  s->have_x = true;
+  return 0;
+}
+
 int brr_session_synthesize(brr_session *s, uint64_t ds, double h2, int64_t n_causal) {
   if (!s) return -1;
   HIPCHK(hipSetDevice(s->device));
-  HIPCHK(launch_synth_x(const_cast<float *>(s->d.X), s->d.ld, s->N, s->M, s->col_offset, ds, s->st));
+  HIPCHK(launch_synth_x(s->d, ds, s->st));
   s->have_x = true;
   // this shard's genetic values X_c beta_c over its causal columns
   if (n_causal < 1) n_causal = std::max<int64_t>(1, std::min<int64_t>(1000, s->M_total / 10));
@@ -632,7 +799,7 @@ int brr_session_synthesize(brr_session *s, uint64_t ds, double h2, int64_t n_cau
     HIPCHK(hipMemcpy(dci, cidx.data(), sizeof(int) * nc, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(dcb, cb.data(), sizeof(double) * nc, hipMemcpyHostToDevice));
   }
-  HIPCHK(launch_synth_y(s->d.X, s->d.ld, s->N, dci, dcb, nc, dy, s->st));
+  HIPCHK(launch_synth_y(s->d, dci, dcb, nc, dy, s->st));
   s->synth_y.assign((size_t)s->N, 0.0);
   HIPCHK(hipStreamSynchronize(s->st));
   HIPCHK(hipMemcpy(s->synth_y.data(), dy, sizeof(double) * s->N, hipMemcpyDeviceToHost));
@@ -958,7 +1125,17 @@ int64_t brr_session_get_vector(brr_session *s, int32_t which, double *out) {
   }
   if (which == 200) {
     std::vector<float> x((size_t)(s->d.ld * s->M));
-    if (int rc = d2h(s, x.data(), s->d.X, (int64_t)x.size())) return rc;
+    if (s->x2bit) {
+      std::vector<uint8_t> c((size_t)(s->d.ldc * s->M));
+      std::vector<float> l((size_t)(4 * s->M));
+      if (int rc = d2h(s, c.data(), s->d.Xc, (int64_t)c.size())) return rc;
+      if (int rc = d2h(s, l.data(), s->d.xlut, (int64_t)l.size())) return rc;
+      for (int64_t j = 0; j < s->M; ++j)
+        for (int64_t i = 0; i < s->d.ld; ++i)
+          x[(size_t)(j * s->d.ld + i)] = l[(size_t)(4 * j + ((c[(size_t)(j * s->d.ldc + (i >> 2))] >> (2 * (i & 3))) & 3))];
+    } else if (int rc = d2h(s, x.data(), s->d.X, (int64_t)x.size())) {
+      return rc;
+    }
     for (int64_t j = 0; j < s->M; ++j) {
       double a = 0;
       for (int64_t i = 0; i < s->d.ld; ++i) a += std::fabs((double)x[(size_t)(j * s->d.ld + i)]);

@@ -28,12 +28,13 @@ class Session:
 
     def __init__(self, model, N, M, *, K=1, groups=1, F=0, M_total=None, col_offset=0,
                  device=0, block_size=0, order_mode=L.ORDER_BLOCKED, shard_rank=0,
-                 shard_count=1, verbose=0, log=None):
+                 shard_count=1, verbose=0, log=None, x_storage=L.X_F32):
         self._keep = []
         self.model, self.N, self.M, self.K, self.G, self.F = model, N, M, K, groups, F
         self.M_total = M if M_total is None else M_total
         self.col_offset = col_offset
-        self.opt = L.options(device, block_size, order_mode, shard_rank, shard_count, verbose, log)
+        self.opt = L.options(device, block_size, order_mode, shard_rank, shard_count, verbose, log,
+                             x_storage)
         self.h = L.lib().brr_session_create(model, N, M, self.M_total, col_offset, K, groups, F,
                                             C.byref(self.opt))
         if not self.h:
@@ -51,6 +52,18 @@ class Session:
         else:
             Xd = np.asfortranarray(X, dtype=np.float64)
             L.check(L.lib().brr_session_upload_x_f64(self.h, _d(Xd), self.N), "upload_x_f64")
+        return self
+
+    def upload_bed(self, bed, bytes_per_col=None):
+        """PLINK .bed body (after the 3 magic bytes) of this shard's markers: uint8 array of
+        M * bytes_per_col bytes (SNP-major), or an (M, bytes_per_col) array."""
+        b = np.ascontiguousarray(bed, dtype=np.uint8)
+        if bytes_per_col is None:
+            bytes_per_col = b.shape[1] if b.ndim == 2 else (self.N + 3) // 4
+        if b.size < self.M * bytes_per_col:
+            raise ValueError("bed holds fewer than M * bytes_per_col bytes")
+        L.check(L.lib().brr_session_upload_bed(self.h, b.ctypes.data_as(C.POINTER(C.c_uint8)), bytes_per_col),
+                "upload_bed")
         return self
 
     def synthesize(self, data_seed=20261015, h2=0.5, n_causal=-1):

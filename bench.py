@@ -124,6 +124,9 @@ def parse():
     ap.add_argument("--cpu-sweeps", type=int, default=3)
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-roofline-events", action="store_true")
+    ap.add_argument("--x-storage", default="f32", choices=["f32", "2bit"],
+                    help="genotype storage on the device: dense f32 (the BASELINE configs) or 2-bit codes "
+                         "+ per-column value tables (SURVEY 8f3; decoded values identical to f32)")
     return ap.parse_args()
 
 
@@ -233,8 +236,13 @@ def main():
     Pl = c1 - c0
     K = 1 if model == L.MODEL_HORSESHOE else len(CVA) + 1
     F = 1 if model == L.MODEL_GROUPS else 0
+    x2 = args.x_storage == "2bit"
     s = B.Session(model, N, Pl, K=K, groups=G, F=F, M_total=P, col_offset=c0, device=local_rank,
-                  block_size=Bsz, order_mode=L.ORDER_BLOCKED, shard_rank=rank, shard_count=world)
+                  block_size=Bsz, order_mode=L.ORDER_BLOCKED, shard_rank=rank, shard_count=world,
+                  x_storage=L.X_2BIT if x2 else L.X_F32)
+    # algorithmic bytes of one pass over this shard's genotypes (f32 values, or 2-bit codes + the
+    # 16-B value table of every column)
+    x_bytes = (N * Pl / 4.0 + 16.0 * Pl) if x2 else 4.0 * N * Pl
     t_setup = time.perf_counter()
     s.synthesize(args.data_seed, 0.5, -1)
     if world > 1:
@@ -307,11 +315,11 @@ def main():
         nbl = (Pl + Bsz - 1) // Bsz
         if fused:
             launches = max(1, tm["stream_launches"] // nbl)
-            bytes_launch = 4.0 * N * Pl
+            bytes_launch = x_bytes
             kname = "k_sweep (fused marker loop: streaming + solver workgroups)"
         else:
             launches = max(1, tm["stream_launches"])
-            bytes_launch = 4.0 * N * Bsz
+            bytes_launch = x_bytes * Bsz / Pl
             kname = "k_stream"
         avg_ms = tm["stream_ms"] / launches
         achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
@@ -323,7 +331,7 @@ def main():
                 "kernel": kname, "avg_launch_us": round(avg_ms * 1e3, 3),
                 "bytes_per_launch": int(bytes_launch),
                 "per_block_us": round(tm["stream_ms"] / max(1, tm["stream_launches"]) * 1e3, 3),
-                "sweep_hbm_gbs": round(4.0 * N * Pl / (ms * 1e-3) / 1e9, 1)}
+                "sweep_hbm_gbs": round(x_bytes / (ms * 1e-3) / 1e9, 1)}
     if args.trace_sweeps:
         # per-sweep wall time and changed markers of a fresh chain's first sweeps (diagnostic)
         tr = []
@@ -366,8 +374,10 @@ def main():
             "metric": METRIC, "value": round(value, 4), "unit": "sweeps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (on-device Binomial(2,f) genotypes, standardised; f32 X, f64 arithmetic)",
-            "config": {"workload": cfg["workload"], "N": N, "P": P, "K": K, "groups": G,
+            "data": ("synthetic (on-device Binomial(2,f) genotypes, standardised; "
+                     + ("2-bit codes + f32 value tables" if x2 else "f32 X") + ", f64 arithmetic)"),
+            "config": {"workload": cfg["workload"] + (" [2-bit genotype storage, SURVEY 8f3]" if x2 else ""),
+                       "x_storage": args.x_storage, "N": N, "P": P, "K": K, "groups": G,
                        "block_size": Bsz, "order": "blocked", "fused_stream_wg": int(s.scalar(104)), "parallelism": f"column-shard x{world}",
                        "setup_s": round(t_setup, 2), "diag": diag},
             "roofline": roof, "cpu_baseline": cpu,

@@ -48,6 +48,14 @@ enum brr_model { BRR_MODEL_V2 = 0, BRR_MODEL_GROUPS = 1, BRR_MODEL_RESTART = 2, 
  *  IDENTITY  markers 0..P-1 in index order every sweep (debugging). */
 enum brr_order { BRR_ORDER_BLOCKED = 0, BRR_ORDER_REFERENCE = 1, BRR_ORDER_IDENTITY = 2 };
 
+/* Device storage of the genotype matrix (no reference counterpart: the reference
+ * keeps a dense f64 Eigen copy, src/BayesRv2.cpp:60).
+ *  F32   dense f32 column-major: any matrix (4 N M bytes, streamed once per sweep).
+ *  2BIT  2-bit codes + a 4-entry f32 value table per column (N M / 4 bytes): for genotype-coded
+ *        columns (at most 3 distinct non-zero values, e.g. scale()d 0/1/2 dosages).  Decoded
+ *        values equal the F32 storage's bit for bit, so a chain is identical under both. */
+enum brr_x_storage { BRR_X_F32 = 0, BRR_X_2BIT = 1 };
+
 typedef void (*brr_log_fn)(const char *msg, void *userdata);
 
 typedef struct brr_options {
@@ -59,7 +67,7 @@ typedef struct brr_options {
   int32_t shard_rank;      /* column shard of this process (default 0) */
   int32_t shard_count;     /* number of column shards / processes (default 1) */
   int32_t verbose;         /* 1 = progress lines "iteration: i" like the reference */
-  int32_t reserved0;
+  int32_t x_storage;       /* enum brr_x_storage (default F32) */
   brr_log_fn log;          /* NULL = stderr */
   void *log_userdata;
 } brr_options;
@@ -106,9 +114,15 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
                                 const brr_options *opt);
 void brr_session_destroy(brr_session *s);
 
-/* X: host column-major N x M (this shard), f64 or f32. */
+/* X: host column-major N x M (this shard), f64 or f32.  With x_storage = BRR_X_2BIT every
+ * column must hold at most 3 distinct non-zero values (error otherwise). */
 int brr_session_upload_x_f64(brr_session *s, const double *X, int64_t ldx);
 int brr_session_upload_x_f32(brr_session *s, const float *X, int64_t ldx);
+/* PLINK .bed body (SNP-major, without the 3 magic bytes) for this shard's M markers,
+ * bytes_per_col >= ceil(N/4) bytes each: genotype = copies of allele 1 (00 -> 2, 10 -> 1, 11 -> 0,
+ * 01 = missing), standardised per column as R's scale() after mean imputation; missing -> 0.
+ * Either storage; with BRR_X_2BIT the codes are stored as they come (no decode on the host). */
+int brr_session_upload_bed(brr_session *s, const uint8_t *bed, int64_t bytes_per_col);
 /* On-device synthetic cohort (DESIGN.md "synthetic data spec"): standardised Binomial(2,f)
  * genotypes for this shard's global columns; Y = standardised X beta + noise computed over
  * all M_total columns' causal set.  Requires shard_count == 1 for Y (else use set_y). */
