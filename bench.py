@@ -166,9 +166,10 @@ def cpu_baseline_child(args):
     print(json.dumps({"t_sweep_sample_s": dt / args.cpu_sweeps, "markers": Pm, "N": N}))
 
 
-def pmc_traffic(args, N, P, B, fused):
+def pmc_traffic(args, N, P, B, fused, x_bytes):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary of the
-    same configuration (profiles/*_pmc.json: FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), or None."""
+    same configuration (profiles/*_pmc.json, written by scripts/pmc_json.py: FETCH_SIZE x2 +
+    WRITE_SIZE, gfx950 correction), or None."""
     import glob
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json"))):
         try:
@@ -176,7 +177,8 @@ def pmc_traffic(args, N, P, B, fused):
         except (OSError, ValueError):
             continue
         if (d.get("config") == args.config and d.get("block_size") == B and fused
-                and d.get("algorithmic_bytes_per_launch") == 4.0 * N * P):
+                and d.get("x_storage", "f32") == args.x_storage
+                and d.get("algorithmic_bytes_per_launch") == x_bytes):
             return d["hbm_bytes_per_launch"], os.path.relpath(f, REPO)
     return None, None
 
@@ -323,7 +325,7 @@ def main():
             kname = "k_stream"
         avg_ms = tm["stream_ms"] / launches
         achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(args, N, Pl, Bsz, fused)
+        traffic, traffic_src = pmc_traffic(args, N, Pl, Bsz, fused, x_bytes)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
