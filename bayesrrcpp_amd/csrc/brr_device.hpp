@@ -99,7 +99,7 @@ struct Dev {
   int64_t slab1_stride, slab2_stride, pend_stride;
   int *pend_idx, *pend_gi;  // [3][B+16]
   double *pend_bo, *pend_bn;
-  int *pend_n;              // [3] padded counts (multiple of 16)
+  int *pend_n;              // [3] padded counts (multiple of 16), then [3] counts before the padding
   double *rslab;
   int *rcnt;
   double *mslab;

@@ -153,7 +153,7 @@ __device__ __forceinline__ void stamp(int *sync, int k) {  // first writer wins
 __device__ __forceinline__ void wait_geq(const int *cnt, int target, int *sync, int where) {
   for (uint32_t n = 0;; ++n) {
     const int v = ld_sc1_int(cnt);
-    if (v >= target) return;
+    if ((int)((unsigned)v - (unsigned)target) >= 0) return;  // cumulative counters: wrap-safe
     if (n == 0 && where == 2) stamp(sync, 6);
     if (n > SPIN_MAX) {
       stamp(sync, 7);
@@ -1845,7 +1845,10 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     st_sc1(pbo + npend + t, 0.0);
     st_sc1(pbn + npend + t, 0.0);
   }
-  if (t == 0) st_sc1_int(d.pend_n + pslot, npad);
+  if (t == 0) {
+    st_sc1_int(d.pend_n + pslot, npad);
+    st_sc1_int(d.pend_n + 3 + pslot, npend);
+  }
   // publish: every storing wave drains its sc1 stores, then the block count (k_stream(s+2))
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1901,40 +1904,56 @@ constexpr int SWEEP_NW = SWEEP_NT / 64;
 #ifndef STREAM_P2
 #define STREAM_P2 3   // the same for 2-bit codes (a byte per column and lane; vmcnt <= 63 caps P CW)
 #endif
+// timing experiments only (results are wrong with either set): skip the streamers' wait for the
+// change list, or the apply of the list
+#ifndef BRR_EXP_NO_WAIT
+#define BRR_EXP_NO_WAIT 0
+#endif
+#ifndef BRR_EXP_NO_APPLY
+#define BRR_EXP_NO_APPLY 0
+#endif
 constexpr int FUSED_GROUP = 16;  // streaming workgroups (slab rows) per level-2 reduction group
 
 // Block `slot`'s change list applied to this workgroup's residual rows:
 // eps_i += x_ij b_old - x_ij b_new in list order (BayesRv2.cpp:191,243).  The rows are cut into
 // 64-row slices, one row per lane, spread over the 8 waves; each wave keeps two batches of 16
 // column loads in flight (the list is padded to a multiple of 16 with neutral entries).
+// msrc != nullptr: also copy the B member indices at msrc to mdst (LDS); loaded before the first
+// barrier, stored after it (the buffer's previous block is then no longer read by any wave).
 template <int XF>
 __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0, int64_t r1, int npass,
                                               double *eps_l, int *s_pidx, double *s_pbo, double *s_pbn,
-                                              int *s_np) {
+                                              int *s_np, const int *msrc = nullptr, int *mdst = nullptr) {
 #pragma clang fp contract(off)
   constexpr int AB = 16;  // columns per batch
   const int t = threadIdx.x, lane = t & 63;
   const int w = t >> 6;
+  const bool mcopy = msrc != nullptr && t < d.B;
+  const int mval = mcopy ? msrc[t] : 0;
   if (t < 64) {
     const int np = ld_sc1_int(d.pend_n + slot);
+    const int nr = ld_sc1_int(d.pend_n + 3 + slot);  // entries before the neutral padding
     const int *pidx = d.pend_idx + slot * d.pend_stride;
     const double *pbo = d.pend_bo + slot * d.pend_stride, *pbn = d.pend_bn + slot * d.pend_stride;
     for (int e = lane; e < np; e += 64) {
-      s_pidx[e] = ld_sc1_int(pidx + e);
+      // neutral padding entries (b_old = b_new = 0) load the last real column again: a cache
+      // hit instead of column 0 from HBM, and no branch in the batched loads
+      s_pidx[e] = ld_sc1_int(pidx + (e < nr ? e : max(nr - 1, 0)));
       s_pbo[e] = ld_sc1(pbo + e);
       s_pbn[e] = ld_sc1(pbn + e);
     }
-    if (lane == 0) *s_np = np;
+    if (lane == 0) s_np[0] = np;
   }
   __syncthreads();
-  const int np = *s_np;
+  const int np = __builtin_amdgcn_readfirstlane(s_np[0]);
   const int64_t ld = d.ld;
   for (int sl = w; sl < npass * 4; sl += SWEEP_NW) {
     const int off = sl * 64 + lane;
     const bool ok = r0 + off < r1;  // rows beyond r1 read row r0 (unconditional loads) and are not stored
     const int64_t rr = ok ? r0 + off : r0;
     const float *Xr = XF ? nullptr : d.X + rr;
-    auto xload = [&](int col) __attribute__((always_inline)) -> float {
+    auto xload = [&](int e) __attribute__((always_inline)) -> float {
+      const int col = s_pidx[e];
       if constexpr (XF) return x_at(d, col, rr);
       else return Xr[(int64_t)col * ld];
     };
@@ -1942,13 +1961,13 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
     float xa[AB], xb[AB];
     if (np > 0) {
 #pragma unroll
-      for (int q = 0; q < AB; ++q) xa[q] = xload(s_pidx[q]);
+      for (int q = 0; q < AB; ++q) xa[q] = xload(q);
     }
     for (int p0 = 0; p0 < np; p0 += 2 * AB) {
       const bool more = p0 + AB < np;
       if (more) {
 #pragma unroll
-        for (int q = 0; q < AB; ++q) xb[q] = xload(s_pidx[p0 + AB + q]);
+        for (int q = 0; q < AB; ++q) xb[q] = xload(p0 + AB + q);
       }
 #pragma unroll
       for (int q = 0; q < AB; ++q) {
@@ -1958,7 +1977,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
       if (!more) break;
       if (p0 + 2 * AB < np) {
 #pragma unroll
-        for (int q = 0; q < AB; ++q) xa[q] = xload(s_pidx[p0 + 2 * AB + q]);
+        for (int q = 0; q < AB; ++q) xa[q] = xload(p0 + 2 * AB + q);
       }
 #pragma unroll
       for (int q = 0; q < AB; ++q) {
@@ -1968,6 +1987,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
     }
     if (ok) eps_l[off] = e;
   }
+  if (mcopy) mdst[t] = mval;
   __syncthreads();
 }
 
@@ -1977,7 +1997,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
 // first item of the block.
 template <int CW, int P, int XF>
 __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int npass, double *eps_l, int *s_pidx,
-                                            double *s_pbo, double *s_pbn, int *s_np, float4 *s_lut) {
+                                            double *s_pbo, double *s_pbn, int *s_np, float4 *s_lut, int *s_mem) {
 #pragma clang fp contract(off)
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -1987,11 +2007,15 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   const bool prof = d.sc->prof_on;
   auto stage_lut = [&](int s) __attribute__((always_inline)) {
     if constexpr (XF) {
-      for (int i = t; i < B; i += SWEEP_NT) s_lut[i] = x_lut(d, d.member[(int64_t)s * B + i]);
+      for (int i = t; i < B; i += SWEEP_NT) s_lut[(s & 1) * B + i] = x_lut(d, d.member[(int64_t)s * B + i]);
     }
   };
   for (int i = t; i < npass * SROWS; i += SWEEP_NT) eps_l[i] = r0 + i < r1 ? d.eps[r0 + i] : 0.0;
   stage_lut(0);
+  // f32 path: the member (column) indices of blocks s and s + 1 live in LDS (s_mem[(s & 1) B ..]),
+  // so an item's loads need no scalar-cache miss first; block s + 1's are copied at boundary s
+  if constexpr (!XF)
+    for (int i = t; i < min(2, nb) * B; i += SWEEP_NT) s_mem[i] = d.member[i];
   __syncthreads();
   const int CPW = B / SWEEP_NW;  // columns per wave
   const int NCH = CPW / CW;      // chunks per wave and block
@@ -2007,15 +2031,23 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     const int s = it / items, rem = it - s * items;
     const int c = rem / npass, p = rem - c * npass;
     const int64_t off = r0 + p * SROWS + 4 * lane < r1 ? r0 + p * SROWS + 4 * lane : r0;
-    const int *mem = d.member + (int64_t)s * B + w * CPW + c * CW;  // wave-uniform: scalar loads
     if constexpr (XF) {
+      const int *mem = d.member + (int64_t)s * B + w * CPW + c * CW;  // wave-uniform: scalar loads
       const uint8_t *base = d.Xc + (off >> 2);
 #pragma unroll
       for (int j = 0; j < CW; ++j) x[j] = base[(int64_t)mem[j] * d.ldc];
     } else {
       const float *base = d.X + off;
+      // (scalar loads of the member indices instead: -6 % at C2, a K$ miss per item)
+      const int4 *m4 = reinterpret_cast<const int4 *>(s_mem + (s & 1) * B + w * CPW + c * CW);
 #pragma unroll
-      for (int j = 0; j < CW; ++j) x[j] = ldg4(base + (int64_t)mem[j] * ld);
+      for (int j = 0; j < CW; j += 4) {
+        const int4 m = m4[j / 4];  // same LDS address in every lane: broadcast
+        x[j + 0] = ldg4(base + (int64_t)__builtin_amdgcn_readfirstlane(m.x) * ld);
+        x[j + 1] = ldg4(base + (int64_t)__builtin_amdgcn_readfirstlane(m.y) * ld);
+        x[j + 2] = ldg4(base + (int64_t)__builtin_amdgcn_readfirstlane(m.z) * ld);
+        x[j + 3] = ldg4(base + (int64_t)__builtin_amdgcn_readfirstlane(m.w) * ld);
+      }
     }
   };
   // register ring of P + 1 items: item it + P is issued before item it is consumed
@@ -2032,15 +2064,20 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     const int s = it / items, rem = it - s * items;
     const int c = rem / npass, p = rem - c * npass;
     const bool blk_end = rem == items - 1;
-    if (XF && rem == 0 && s == 1) {  // (every wave passed block 0's closing barrier)
-      stage_lut(1);
+    if (rem == 0 && s == 1) {
+      if constexpr (XF) {
+        stage_lut(1);  // (buffer 1: no wave reads it before the barrier)
+      } else if (nb > 2) {
+        __syncthreads();  // every wave is done issuing block 0's items
+        for (int i = t; i < B; i += SWEEP_NT) s_mem[i] = d.member[2 * B + i];
+      }
       __syncthreads();
     }
     if (rem == 0 && s >= 2) {
       // block boundary: bring the residual rows from E_{s-2} to E_{s-1} (block s-2's changes);
       // the value tables of block s go to LDS before apply_pending's first barrier
       stage_lut(s);
-      if (t == 0) {
+      if (t == 0 && !BRR_EXP_NO_WAIT) {
         wait_geq(d.sync + SY_PEND, d.sbase + s - 1, d.sync, 2);
         if (prof) {
           tr_first(d, s, TR_PEND_FIRST);
@@ -2050,7 +2087,9 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
           t_mark = tn;
         }
       }
-      apply_pending<XF>(d, (s - 2) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np);
+      if (!BRR_EXP_NO_APPLY)
+        apply_pending<XF>(d, (s - 2) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np,
+                          (!XF && s + 1 < nb) ? d.member + (int64_t)(s + 1) * B : nullptr, s_mem + ((s + 1) & 1) * B);
       if (prof && t == 0) {
         tr_last(d, s, TR_APPLY_LAST);
         if (s == nb / 2) d.trace[(int64_t)nb * 16 + 1024 + g] = wall_clock64();  // per-workgroup probe
@@ -2067,7 +2106,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
       float4 xv;
-      if constexpr (XF) xv = x_decode4(xq[0][j], s_lut[w * CPW + c * CW + j]);
+      if constexpr (XF) xv = x_decode4(xq[0][j], s_lut[(s & 1) * B + w * CPW + c * CW + j]);
       else xv = xq[0][j];
       v[j] += (((double)xv.x * e0 + (double)xv.y * e1) + (double)xv.z * e2) + (double)xv.w * e3;
     }
@@ -2094,15 +2133,17 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     if (blk_end) {
       // block done.  The partial-dot stores were issued before the next item's loads, so
       // waiting until only those loads are outstanding drains the stores (vmcnt counts in
-      // issue order) without draining the prefetch; then one arrival on the group counter
-      // for the reducer workgroup.
+      // issue order) without draining the prefetch.
       asm volatile("" ::: "memory");
       if (it + P < total) issue(it + P, xq[P - 1]);
       if (it + P < total) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P * CW) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // then one arrival on the group counter for the reducer workgroup (one per workgroup:
+      // per-wave arrivals measured 1.6x slower, contention on the group counters)
       __syncthreads();
-      if (t == 0) {
+      if (t == 0)
         __hip_atomic_fetch_add(d.cnt1 + (s & 1) * d.NG + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == 0) {
         if (prof) {
           tr_first(d, s, TR_ITEMS_FIRST);
           tr_last(d, s, TR_ITEMS_LAST);
@@ -2172,7 +2213,7 @@ template <bool HS, int B, int XF>
 __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int nslot, int nsg, int rpw, int npass,
                                                         int nred) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ int s_np;
+  __shared__ int s_np[2];
   // residency census: every workgroup must be running before any waits on another
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(d.sync + SY_ARRIVE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2184,15 +2225,15 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
   } else if ((int)blockIdx.x > nsg) {
     reduce_role(d, (int)blockIdx.x - 1 - nsg, nsg, nred, d.sc->prof_on);
   } else {
-    // streamer LDS: residual rows, [value tables of the block (2-bit codes)], the change list
-    // being applied (fused_config)
+    // streamer LDS: residual rows, [value tables of two blocks (2-bit codes)], the change list
+    // being applied, member indices of two blocks (fused_config)
     double *eps_l = reinterpret_cast<double *>(smem);
     float4 *s_lut = reinterpret_cast<float4 *>(eps_l + (int64_t)npass * SROWS);
-    double *s_pbo = reinterpret_cast<double *>(s_lut + (XF ? d.B : 0)), *s_pbn = s_pbo + (d.B + 16);
+    double *s_pbo = reinterpret_cast<double *>(s_lut + (XF ? 2 * d.B : 0)), *s_pbn = s_pbo + (d.B + 16);
     int *s_pidx = reinterpret_cast<int *>(s_pbn + (d.B + 16));
+    int *s_mem = s_pidx + (d.B + 16);  // 16-B aligned: B + 16 is a multiple of 4
     stream_role<STREAM_CW, XF ? STREAM_P2 : STREAM_P, XF>(d, (int)blockIdx.x - 1, rpw, npass, eps_l, s_pidx, s_pbo,
-                                                         s_pbn, &s_np,
-                                         s_lut);
+                                                         s_pbn, s_np, s_lut, s_mem);
   }
 }
 
@@ -2505,10 +2546,10 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   if (fixed + 8 * (size_t)d.B > budget) return false;
   const int nslot = (int)std::min<size_t>((size_t)solve_max_slots(d.B, SWEEP_NT), (budget - fixed) / (8 * (size_t)d.B));
   if ((size_t)nslot * d.B < solve_scratch_doubles(d.B, SWEEP_NT)) return false;
-  // streamers: residual rows, [the block's value tables], the change list (indices, old and new
-  // betas) in LDS
-  const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double) + (xf ? (size_t)d.B * 16 : 0) +
-                           (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int));
+  // streamers: residual rows, [the value tables of two blocks], the change list (indices, old and
+  // new betas), the member indices of two blocks in LDS
+  const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double) + (xf ? (size_t)d.B * 32 : 0) +
+                           (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int)) + 2 * sizeof(int) * d.B;
   const size_t lds = std::max(fixed + (size_t)nslot * 8 * d.B, eps_bytes);
   if (lds > budget) return false;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) != hipSuccess) return false;

@@ -523,7 +523,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   rc |= s->alloc(&d.pend_gi, 3 * d.pend_stride);
   rc |= s->alloc(&d.pend_bo, 3 * d.pend_stride);
   rc |= s->alloc(&d.pend_bn, 3 * d.pend_stride);
-  rc |= s->alloc(&d.pend_n, 3);
+  rc |= s->alloc(&d.pend_n, 6);  // [3] padded list lengths, [3] entries before the padding
   rc |= s->alloc(&d.trace, (int64_t)s->nb * 16 + 5120);  // + per-workgroup probes and totals
   d.nbB = (int64_t)s->nb * B;
   rc |= s->alloc(&d.mc, d.nbB * (3 + 2 * std::max(K, 1)));
@@ -541,7 +541,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   bool ok = hipMemsetAsync(d.cnt1, 0, sizeof(int) * 2 * d.NG * NC, s->st) == hipSuccess &&
             hipMemsetAsync(d.sync, 0, sizeof(int) * SY_WORDS, s->st) == hipSuccess &&
             hipMemsetAsync(d.pend_gi, 0, sizeof(int) * 3 * d.pend_stride, s->st) == hipSuccess &&
-            hipMemsetAsync(d.pend_n, 0, sizeof(int) * 3, s->st) == hipSuccess &&
+            hipMemsetAsync(d.pend_n, 0, sizeof(int) * 6, s->st) == hipSuccess &&
             hipMemsetAsync(d.eps, 0, sizeof(double) * d.ld, s->st) == hipSuccess &&
             hipMemsetAsync(d.eps2, 0, sizeof(double) * d.ld, s->st) == hipSuccess &&
             hipMemsetAsync(d.slab2, 0, sizeof(double) * 2 * d.slab2_stride, s->st) == hipSuccess &&
