@@ -80,6 +80,7 @@ struct Dev {
   const uint8_t *Xc;   // 2-bit genotype codes (BRR_X_2BIT), else nullptr: column j at Xc + j ldc,
                        // row i in bits 2(i&3)..2(i&3)+1 of byte i>>2 (PLINK .bed packing)
   const float *xlut;   // [M][4] value of each code of column j (padding rows decode to 0)
+  float4 *xlut_ord;    // [nb B] value tables in this sweep's visit order (k_lut_order)
   int64_t ldc;         // bytes per code column = ld / 4
   const double *Y, *fixed, *cva;
   const int *gAssign;
@@ -98,6 +99,7 @@ struct Dev {
   int abase;                // persistent streamer arrivals before this sweep (SY_ARRIVE epoch)
   int64_t slab1_stride, slab2_stride, pend_stride;
   int *pend_idx, *pend_gi;  // [3][B+16]
+  int *pend_pos;            // [3][B+16] visit position of each change within its block
   double *pend_bo, *pend_bn;
   int *pend_n;              // [3] padded counts (multiple of 16), then [3] counts before the padding
   double *rslab;

@@ -501,6 +501,13 @@ __global__ void k_perm_within(Dev d, uint32_t it, int identity) {
   if (threadIdx.x == 0) { d.bsz[s] = size; d.gblk[s] = b; }
 }
 
+// 2-bit storage: the value tables in visit order, so a streaming workgroup stages a block's
+// tables with one independent 16-B load per position.
+__global__ __launch_bounds__(256) void k_lut_order(Dev d) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q < d.nbB) d.xlut_ord[q] = x_lut(d, d.member[q]);
+}
+
 // ------------------------------------------------------------------------------------
 // Fixed effects (BayesRv2Groups.cpp:216-225), one workgroup, sequential over F columns.
 __global__ __launch_bounds__(1024) void k_fixed(Dev d, uint32_t it, int perm_on_device) {
@@ -1802,6 +1809,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   // 4) write back, compact the changed markers into this block's list (position order)
   const int pslot = s % 3;
   int *pidx = d.pend_idx + pslot * d.pend_stride, *pgi = d.pend_gi + pslot * d.pend_stride;
+  int *ppos = d.pend_pos + pslot * d.pend_stride;
   double *pbo = d.pend_bo + pslot * d.pend_stride, *pbn = d.pend_bn + pslot * d.pend_stride;
   base = 0;
 #pragma unroll
@@ -1831,6 +1839,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       const int idx = pre + __popcll(bal & ((1ull << lane) - 1ull));
       st_sc1_int(pidx + idx, m);
       st_sc1_int(pgi + idx, Lgi[pos]);
+      st_sc1_int(ppos + idx, pos);
       st_sc1(pbo + idx, bov);
       st_sc1(pbn + idx, bnv);
     }
@@ -1842,6 +1851,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   if (npend + t < npad) {  // neutral padding: eps + x*0 - x*0 == eps exactly, delta = 0
     st_sc1_int(pidx + npend + t, 0);
     st_sc1_int(pgi + npend + t, 0);
+    st_sc1_int(ppos + npend + t, 0);
     st_sc1(pbo + npend + t, 0.0);
     st_sc1(pbn + npend + t, 0.0);
   }
@@ -1920,16 +1930,25 @@ constexpr int FUSED_GROUP = 16;  // streaming workgroups (slab rows) per level-2
 // column loads in flight (the list is padded to a multiple of 16 with neutral entries).
 // msrc != nullptr: also copy the B member indices at msrc to mdst (LDS); loaded before the first
 // barrier, stored after it (the buffer's previous block is then no longer read by any wave).
+// ccode != nullptr (2-bit storage): the code bytes of the block being applied are in LDS
+// (stream_role's code cache, ccode[pos * npass * 64 + row / 4]); s_ppos receives the positions.
+// 2-bit storage: lsrc / ldst stage the next block's value tables the same way; lutb = the value
+// tables of the block being applied (LDS, by visit position, s_ppos receives the positions).
 template <int XF>
 __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0, int64_t r1, int npass,
                                               double *eps_l, int *s_pidx, double *s_pbo, double *s_pbn,
-                                              int *s_np, const int *msrc = nullptr, int *mdst = nullptr) {
+                                              int *s_np, const int *msrc = nullptr, int *mdst = nullptr,
+                                              const uint8_t *ccode = nullptr, int *s_ppos = nullptr,
+                                              const float4 *lsrc = nullptr, float4 *ldst = nullptr,
+                                              const float4 *lutb = nullptr) {
 #pragma clang fp contract(off)
   constexpr int AB = 16;  // columns per batch
   const int t = threadIdx.x, lane = t & 63;
   const int w = t >> 6;
   const bool mcopy = msrc != nullptr && t < d.B;
   const int mval = mcopy ? msrc[t] : 0;
+  const bool lcopy = XF && lsrc != nullptr && t < d.B;
+  const float4 lval = lcopy ? lsrc[t] : make_float4(0.f, 0.f, 0.f, 0.f);
   if (t < 64) {
     const int np = ld_sc1_int(d.pend_n + slot);
     const int nr = ld_sc1_int(d.pend_n + 3 + slot);  // entries before the neutral padding
@@ -1938,7 +1957,9 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
     for (int e = lane; e < np; e += 64) {
       // neutral padding entries (b_old = b_new = 0) load the last real column again: a cache
       // hit instead of column 0 from HBM, and no branch in the batched loads
-      s_pidx[e] = ld_sc1_int(pidx + (e < nr ? e : max(nr - 1, 0)));
+      const int es = e < nr ? e : max(nr - 1, 0);
+      s_pidx[e] = ld_sc1_int(pidx + es);
+      if (XF) s_ppos[e] = ld_sc1_int(d.pend_pos + slot * d.pend_stride + es);
       s_pbo[e] = ld_sc1(pbo + e);
       s_pbn[e] = ld_sc1(pbn + e);
     }
@@ -1952,9 +1973,14 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
     const bool ok = r0 + off < r1;  // rows beyond r1 read row r0 (unconditional loads) and are not stored
     const int64_t rr = ok ? r0 + off : r0;
     const float *Xr = XF ? nullptr : d.X + rr;
+    const int cb = npass * 64;  // code bytes per column in the cache
     auto xload = [&](int e) __attribute__((always_inline)) -> float {
       const int col = s_pidx[e];
-      if constexpr (XF) return x_at(d, col, rr);
+      if constexpr (XF) {
+        const int pos = s_ppos[e];
+        const uint32_t byte = ccode ? (uint32_t)ccode[pos * cb + (off >> 2)] : (uint32_t)d.Xc[col * d.ldc + (rr >> 2)];
+        return x_sel(lutb[pos], byte >> (2 * ((ccode ? off : rr) & 3)));
+      }
       else return Xr[(int64_t)col * ld];
     };
     double e = eps_l[off];
@@ -1988,6 +2014,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
     if (ok) eps_l[off] = e;
   }
   if (mcopy) mdst[t] = mval;
+  if (lcopy) ldst[t] = lval;
   __syncthreads();
 }
 
@@ -1997,7 +2024,8 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
 // first item of the block.
 template <int CW, int P, int XF>
 __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int npass, double *eps_l, int *s_pidx,
-                                            double *s_pbo, double *s_pbn, int *s_np, float4 *s_lut, int *s_mem) {
+                                            double *s_pbo, double *s_pbn, int *s_np, float4 *s_lut, int *s_mem,
+                                            uint8_t *s_codes) {
 #pragma clang fp contract(off)
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -2005,13 +2033,16 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   const int B = d.B, nb = d.nb;
   const int64_t ld = d.ld;
   const bool prof = d.sc->prof_on;
+  // 2-bit storage: the value tables of blocks s - 2 .. s + 1 in LDS (buffer s & 3): block s + 1's
+  // are staged at boundary s (inside the apply), block s - 2's serve the apply
   auto stage_lut = [&](int s) __attribute__((always_inline)) {
     if constexpr (XF) {
-      for (int i = t; i < B; i += SWEEP_NT) s_lut[(s & 1) * B + i] = x_lut(d, d.member[(int64_t)s * B + i]);
+      for (int i = t; i < B; i += SWEEP_NT) s_lut[(s & 3) * B + i] = d.xlut_ord[(int64_t)s * B + i];
     }
   };
   for (int i = t; i < npass * SROWS; i += SWEEP_NT) eps_l[i] = r0 + i < r1 ? d.eps[r0 + i] : 0.0;
   stage_lut(0);
+  if (nb > 1) stage_lut(1);
   // f32 path: the member (column) indices of blocks s and s + 1 live in LDS (s_mem[(s & 1) B ..]),
   // so an item's loads need no scalar-cache miss first; block s + 1's are copied at boundary s
   if constexpr (!XF)
@@ -2019,6 +2050,11 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   __syncthreads();
   const int CPW = B / SWEEP_NW;  // columns per wave
   const int NCH = CPW / CW;      // chunks per wave and block
+  // 2-bit storage with room in LDS: the code bytes of this workgroup's rows of the last three
+  // blocks (buffer s % 3), so the change list of block s - 2 is applied from LDS, not HBM
+  auto cache_of = [&](int s) __attribute__((always_inline)) -> const uint8_t * {
+    return (XF && s_codes) ? s_codes + (int64_t)(s % 3) * B * (npass * 64) : nullptr;
+  };
   const int items = NCH * npass; // (chunk, pass) items per wave and block
   const int total = items * nb;
   const int grp = g / FUSED_GROUP;
@@ -2066,7 +2102,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     const bool blk_end = rem == items - 1;
     if (rem == 0 && s == 1) {
       if constexpr (XF) {
-        stage_lut(1);  // (buffer 1: no wave reads it before the barrier)
+        if (nb > 2) stage_lut(2);  // (buffer 2: no wave reads it before the barrier)
       } else if (nb > 2) {
         __syncthreads();  // every wave is done issuing block 0's items
         for (int i = t; i < B; i += SWEEP_NT) s_mem[i] = d.member[2 * B + i];
@@ -2074,9 +2110,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       __syncthreads();
     }
     if (rem == 0 && s >= 2) {
-      // block boundary: bring the residual rows from E_{s-2} to E_{s-1} (block s-2's changes);
-      // the value tables of block s go to LDS before apply_pending's first barrier
-      stage_lut(s);
+      // block boundary: bring the residual rows from E_{s-2} to E_{s-1} (block s-2's changes)
       if (t == 0 && !BRR_EXP_NO_WAIT) {
         wait_geq(d.sync + SY_PEND, d.sbase + s - 1, d.sync, 2);
         if (prof) {
@@ -2089,7 +2123,9 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       }
       if (!BRR_EXP_NO_APPLY)
         apply_pending<XF>(d, (s - 2) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np,
-                          (!XF && s + 1 < nb) ? d.member + (int64_t)(s + 1) * B : nullptr, s_mem + ((s + 1) & 1) * B);
+                          (!XF && s + 1 < nb) ? d.member + (int64_t)(s + 1) * B : nullptr, s_mem + ((s + 1) & 1) * B,
+                          cache_of(s - 2), s_mem, (XF && s + 1 < nb) ? d.xlut_ord + (int64_t)(s + 1) * B : nullptr,
+                          s_lut + ((s + 1) & 3) * B, s_lut + ((s - 2) & 3) * B);
       if (prof && t == 0) {
         tr_last(d, s, TR_APPLY_LAST);
         if (s == nb / 2) d.trace[(int64_t)nb * 16 + 1024 + g] = wall_clock64();  // per-workgroup probe
@@ -2106,8 +2142,13 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
       float4 xv;
-      if constexpr (XF) xv = x_decode4(xq[0][j], s_lut[(s & 1) * B + w * CPW + c * CW + j]);
-      else xv = xq[0][j];
+      if constexpr (XF) {
+        xv = x_decode4(xq[0][j], s_lut[(s & 3) * B + w * CPW + c * CW + j]);
+        // code cache: block s's bytes at position w CPW + c CW + j, row byte p 64 + lane
+        if (s_codes) s_codes[((s % 3) * B + w * CPW + c * CW + j) * (npass * 64) + p * 64 + lane] = (uint8_t)xq[0][j];
+      } else {
+        xv = xq[0][j];
+      }
       v[j] += (((double)xv.x * e0 + (double)xv.y * e1) + (double)xv.z * e2) + (double)xv.w * e3;
     }
 #pragma unroll
@@ -2163,9 +2204,13 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   }
   // end of sweep: the last two blocks' changes, then the residual rows back to HBM
   if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + nb, d.sync, 4);
-  if (nb >= 2) apply_pending<XF>(d, (nb - 2) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np);
-  else __syncthreads();
-  apply_pending<XF>(d, (nb - 1) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np);
+  if (nb >= 2)
+    apply_pending<XF>(d, (nb - 2) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, nullptr, nullptr,
+                      cache_of(nb - 2), s_mem, nullptr, nullptr, s_lut + ((nb - 2) & 3) * B);
+  else
+    __syncthreads();
+  apply_pending<XF>(d, (nb - 1) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, nullptr, nullptr,
+                    cache_of(nb - 1), s_mem, nullptr, nullptr, s_lut + ((nb - 1) & 3) * B);
   for (int i = t; i < npass * SROWS; i += SWEEP_NT)
     if (r0 + i < r1) d.eps[r0 + i] = eps_l[i];
 }
@@ -2211,7 +2256,7 @@ __device__ __forceinline__ void solver_role(const Dev &d, uint32_t it, int nslot
 
 template <bool HS, int B, int XF>
 __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int nslot, int nsg, int rpw, int npass,
-                                                        int nred) {
+                                                        int nred, int ccache) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_np[2];
   // residency census: every workgroup must be running before any waits on another
@@ -2225,15 +2270,17 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
   } else if ((int)blockIdx.x > nsg) {
     reduce_role(d, (int)blockIdx.x - 1 - nsg, nsg, nred, d.sc->prof_on);
   } else {
-    // streamer LDS: residual rows, [value tables of two blocks (2-bit codes)], the change list
+    // streamer LDS: residual rows, [value tables of four blocks (2-bit codes)], the change list
     // being applied, member indices of two blocks (fused_config)
     double *eps_l = reinterpret_cast<double *>(smem);
     float4 *s_lut = reinterpret_cast<float4 *>(eps_l + (int64_t)npass * SROWS);
-    double *s_pbo = reinterpret_cast<double *>(s_lut + (XF ? 2 * d.B : 0)), *s_pbn = s_pbo + (d.B + 16);
+    double *s_pbo = reinterpret_cast<double *>(s_lut + (XF ? 4 * d.B : 0)), *s_pbn = s_pbo + (d.B + 16);
     int *s_pidx = reinterpret_cast<int *>(s_pbn + (d.B + 16));
     int *s_mem = s_pidx + (d.B + 16);  // 16-B aligned: B + 16 is a multiple of 4
+    // (2-bit storage: s_mem holds the change positions instead; then the code cache)
+    uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_mem + 2 * d.B) : nullptr;
     stream_role<STREAM_CW, XF ? STREAM_P2 : STREAM_P, XF>(d, (int)blockIdx.x - 1, rpw, npass, eps_l, s_pidx, s_pbo,
-                                                         s_pbn, s_np, s_lut, s_mem);
+                                                         s_pbn, s_np, s_lut, s_mem, s_codes);
   }
 }
 
@@ -2481,6 +2528,11 @@ hipError_t launch_perm(const Dev &d, uint32_t it, int shard, bool identity, hipS
   return hipGetLastError();
 }
 
+hipError_t launch_lut_order(const Dev &d, hipStream_t st) {
+  hipLaunchKernelGGL(k_lut_order, dim3(cdiv64(d.nbB, 256)), dim3(256), 0, st, d);
+  return hipGetLastError();
+}
+
 hipError_t launch_fixed(const Dev &d, uint32_t it, bool perm_on_device, hipStream_t st) {
   hipLaunchKernelGGL(k_fixed, dim3(1), dim3(1024), 0, st, d, it, perm_on_device ? 1 : 0);
   return hipGetLastError();
@@ -2548,9 +2600,11 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   if ((size_t)nslot * d.B < solve_scratch_doubles(d.B, SWEEP_NT)) return false;
   // streamers: residual rows, [the value tables of two blocks], the change list (indices, old and
   // new betas), the member indices of two blocks in LDS
-  const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double) + (xf ? (size_t)d.B * 32 : 0) +
+  const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double) + (xf ? (size_t)d.B * 64 : 0) +
                            (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int)) + 2 * sizeof(int) * d.B;
-  const size_t lds = std::max(fixed + (size_t)nslot * 8 * d.B, eps_bytes);
+  const size_t code_bytes = xf ? (size_t)3 * d.B * npass * 64 : 0;
+  const bool ccache = xf && eps_bytes + code_bytes <= budget && !getenv("BRR_NO_CODE_CACHE");
+  const size_t lds = std::max(fixed + (size_t)nslot * 8 * d.B, eps_bytes + (ccache ? code_bytes : 0));
   if (lds > budget) return false;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) != hipSuccess) return false;
   int per_cu = 0;
@@ -2563,6 +2617,7 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   cfg->ngroups = nred;
   cfg->nred = nred;
   cfg->lds = lds;
+  cfg->ccache = ccache ? 1 : 0;
   return true;
 }
 
@@ -2572,9 +2627,9 @@ hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipS
 #define BRR_SWEEP_LAUNCH(HSV, BV)                                                                                  \
   do {                                                                                                             \
     if (xf) hipLaunchKernelGGL((k_sweep<HSV, BV, 1>), grid, blk, c.lds, st, d, it, c.nslot, c.nsg, c.rpw, c.npass, \
-                               c.nred);                                                                            \
+                               c.nred, c.ccache);                                                                  \
     else hipLaunchKernelGGL((k_sweep<HSV, BV, 0>), grid, blk, c.lds, st, d, it, c.nslot, c.nsg, c.rpw, c.npass,    \
-                            c.nred);                                                                               \
+                            c.nred, 0);                                                                            \
   } while (0)
   switch (d.B) {
     case 128: if (hs) BRR_SWEEP_LAUNCH(true, 128); else BRR_SWEEP_LAUNCH(false, 128); break;

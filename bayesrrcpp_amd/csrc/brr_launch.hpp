@@ -16,6 +16,7 @@ hipError_t launch_synth_x(const Dev &d, uint64_t ds, hipStream_t st);
 hipError_t launch_synth_y(const Dev &d, const int *cidx, const double *cb, int nc, double *y, hipStream_t st);
 hipError_t launch_cast_x(const void *src, bool is_f64, int64_t lds, float *dst, int64_t ldd,
                          int64_t N, int64_t M, hipStream_t st);
+hipError_t launch_lut_order(const Dev &d, hipStream_t st);
 hipError_t launch_gram(const Dev &d, int shift, double *G, double *GT, hipStream_t st);
 hipError_t launch_xsq(const Dev &d, hipStream_t st);
 hipError_t launch_rows(const Dev &d, int flags, const double *deps_in, hipStream_t st,
@@ -28,6 +29,7 @@ hipError_t launch_stream(const Dev &d, int s, const double *eps_in, double *eps_
 hipError_t launch_prep(const Dev &d, uint32_t it, hipStream_t st);
 struct FusedCfg {
   int nsg = 0, rpw = 0, npass = 0, nslot = 0, ngroups = 0, nred = 0;
+  int ccache = 0;  // 2-bit storage: the streamers keep the last three blocks' code bytes in LDS
   size_t lds = 0;
 };
 bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg);

@@ -266,6 +266,7 @@ int do_sweep_local(brr_session *s) {
   } else {
     HIPCHK(launch_perm(d, it, s->shard, true, s->st));
   }
+  if (d.Xc) HIPCHK(launch_lut_order(d, s->st));
   if (s->model == MODEL_GROUPS && s->F > 0)
     HIPCHK(launch_fixed(d, it, s->order_mode == BRR_ORDER_BLOCKED, s->st));
   if (sharded)
@@ -485,6 +486,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   if (s->x2bit) {
     rc |= s->alloc(const_cast<uint8_t **>(&d.Xc), d.ldc * M);
     rc |= s->alloc(const_cast<float **>(&d.xlut), 4 * M);
+    rc |= s->alloc(reinterpret_cast<float **>(&d.xlut_ord), 4 * (int64_t)s->nb * B);
   } else {
     rc |= s->alloc(const_cast<float **>(&d.X), d.ld * M);
   }
@@ -520,6 +522,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   rc |= s->alloc(&d.cnt1, 2 * (int64_t)d.NG * NC);
   rc |= s->alloc(&d.sync, SY_WORDS);
   rc |= s->alloc(&d.pend_idx, 3 * d.pend_stride);
+  rc |= s->alloc(&d.pend_pos, 3 * d.pend_stride);
   rc |= s->alloc(&d.pend_gi, 3 * d.pend_stride);
   rc |= s->alloc(&d.pend_bo, 3 * d.pend_stride);
   rc |= s->alloc(&d.pend_bn, 3 * d.pend_stride);
@@ -548,6 +551,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
             hipMemsetAsync(d.member, 0, sizeof(int) * s->nb * B, s->st) == hipSuccess &&
             hipMemsetAsync(d.gidx, 0, sizeof(int) * s->nb * B, s->st) == hipSuccess &&
             hipMemsetAsync(d.pend_idx, 0, sizeof(int) * 3 * d.pend_stride, s->st) == hipSuccess &&
+            hipMemsetAsync(d.pend_pos, 0, sizeof(int) * 3 * d.pend_stride, s->st) == hipSuccess &&
             hipMemsetAsync(d.pend_bo, 0, sizeof(double) * 3 * d.pend_stride, s->st) == hipSuccess &&
             hipMemsetAsync(d.pend_bn, 0, sizeof(double) * 3 * d.pend_stride, s->st) == hipSuccess &&
             hipMemsetAsync(d.rcnt, 0, sizeof(int), s->st) == hipSuccess &&
@@ -1071,6 +1075,7 @@ int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
     case 101: *out = (double)sc.n_changed; return 0;
     case 102: *out = (double)sc.prof_on; return 0;
     case 104: *out = (double)s->fused.nsg; return 0;  // fused sweep: streaming workgroups (0 = per-block)
+    case 105: *out = (double)s->fused.ccache; return 0;  // fused sweep: 2-bit code cache in LDS
     case 110: case 111: case 112: case 113: case 114: case 115: case 116: case 117: case 118: case 119:
     case 120: case 121:
       *out = (double)sc.prof[which - 110]; return 0;

@@ -166,3 +166,31 @@ def test_2bit_rejects_non_genotype_columns(brr, require_gpu):
     X[7, 3] = 0.5  # a fourth non-zero value in column 3
     with pytest.raises(L.BrrError, match="column 3"):
         s.upload_x(X)
+
+
+@pytest.mark.parametrize("model,cap", [(0, None), (0, 30), (3, 30), (1, 7)])
+def test_2bit_code_cache_midsize(brr, require_gpu, monkeypatch, model, cap):
+    """The streamers' LDS cache of the last three blocks' code bytes (the change list of block s-2
+    is applied from it): several row passes per workgroup, ragged last workgroup, every model.
+    Identical to the f32 chain and to the 2-bit chain that re-reads the codes from HBM."""
+    from bayesrrcpp_amd import _lib as L
+    from oracle import oracle as O
+    if cap:
+        monkeypatch.setenv("BRR_STREAM_WG", str(cap))
+    N, P, B = 20003, 1536, 128
+    X, Y, _ = O.synth_cohort(20261015, N, P, h2=0.5, n_causal=60)
+    G = 4 if model == L.MODEL_GROUPS else 1
+    gA = (np.arange(P) * G // P).astype(np.int32) if G > 1 else None
+    a = _session(brr, L, model, X, Y, B, L.X_F32, G, gA)
+    b = _session(brr, L, model, X, Y, B, L.X_2BIT, G, gA)
+    monkeypatch.setenv("BRR_NO_CODE_CACHE", "1")
+    c = _session(brr, L, model, X, Y, B, L.X_2BIT, G, gA)
+    assert a.scalar(104) > 0 and b.scalar(104) == a.scalar(104) == c.scalar(104)  # fused sweep
+    # code cache on / off (12 row passes per workgroup at cap 7: three blocks of codes do not fit
+    # in LDS, the apply re-reads them from HBM)
+    assert b.scalar(105) == (0 if cap == 7 else 1) and c.scalar(105) == 0
+    for it in range(3):
+        for s in (a, b, c):
+            s.sweep(1)
+        _identical(a, b, L, model, f"cache model={model} cap={cap} it={it}")
+        _identical(a, c, L, model, f"no cache model={model} cap={cap} it={it}")
