@@ -150,6 +150,9 @@ __device__ __forceinline__ void stamp(int *sync, int k) {  // first writer wins
   atomicCAS(ts, 0ull, (unsigned long long)wall_clock64());
 }
 
+#ifndef BRR_SPIN_SLEEP
+#define BRR_SPIN_SLEEP 8  // s_sleep units (64 clocks) between polls of a hand-over counter
+#endif
 __device__ __forceinline__ void wait_geq(const int *cnt, int target, int *sync, int where) {
   for (uint32_t n = 0;; ++n) {
     const int v = ld_sc1_int(cnt);
@@ -166,7 +169,7 @@ __device__ __forceinline__ void wait_geq(const int *cnt, int target, int *sync, 
       return;
     }
     if ((n & 255) == 255 && ld_sc1_int(sync + SY_ERR)) return;  // an earlier wait already failed
-    __builtin_amdgcn_s_sleep(8);
+    __builtin_amdgcn_s_sleep(BRR_SPIN_SLEEP);
   }
 }
 

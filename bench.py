@@ -113,7 +113,7 @@ def parse():
     ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--P", type=int, default=None)
     ap.add_argument("--block-size", type=int, default=0,
-                    help="marker block B; 0 = the library's automatic choice (512 BayesR family, 128 Horseshoe)")
+                    help="marker block B; 0 = the library's automatic choice (512 V2, 128 Groups and Horseshoe)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--data-seed", type=int, default=20261015)
     ap.add_argument("--profile-solve", action="store_true", help="k_solve phase timers (diag)")
@@ -229,7 +229,7 @@ def main():
     N = args.N or cfg["N"]
     P = args.P or cfg["P"]
     model = {"v2": L.MODEL_V2, "groups": L.MODEL_GROUPS, "hs": L.MODEL_HORSESHOE}[cfg["model"]]
-    Bsz = args.block_size or (128 if model == L.MODEL_HORSESHOE else 512)
+    Bsz = args.block_size or (128 if model in (L.MODEL_HORSESHOE, L.MODEL_GROUPS) else 512)  # = libbrr's automatic B
     G = cfg["groups"]
     # contiguous block shards
     nb = (P + Bsz - 1) // Bsz

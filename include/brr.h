@@ -62,7 +62,7 @@ typedef struct brr_options {
   int32_t abi_version;     /* BRR_ABI_VERSION */
   int32_t device;          /* HIP device ordinal (default 0) */
   int32_t block_size;      /* marker block B: 64, 128, 256 or 512; 0 (default) = automatic:
-                              512 for the BayesR family, 128 for the Horseshoe */
+                              512 for V2 / restart, 128 for Groups and the Horseshoe */
   int32_t order_mode;      /* enum brr_order (default BLOCKED) */
   int32_t shard_rank;      /* column shard of this process (default 0) */
   int32_t shard_count;     /* number of column shards / processes (default 1) */
