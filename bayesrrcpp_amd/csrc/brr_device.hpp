@@ -58,12 +58,21 @@ struct Hyper {
 // cumulative over the session (epochs), so nothing is ever reset inside a kernel.
 enum SyncWord : int {
   SY_PEND = 0,     // blocks whose k_solve has published its change list (session total)
-  SY_GDONE = 32,   // + 32 * parity: level-2 reduction groups completed (session total)
-  SY_ERR = 96,     // a bounded wait expired; SY_ERR + 1..4: site, target, value seen, workgroup
-  SY_ARRIVE = 128, // persistent streamer workgroups that started (session total)
-  SY_TS = 160,     // diagnostics: 64-bit wall-clock stamps (see brr_session.cpp)
-  SY_WORDS = 192
+  SY_GDONE = 32,   // + 32 * (s % NPAR): level-2 reduction groups completed (session total)
+  SY_ERR = 128,    // a bounded wait expired; SY_ERR + 1..4: site, target, value seen, workgroup
+  SY_ARRIVE = 160, // persistent streamer workgroups that started (session total)
+  SY_TS = 192,     // diagnostics: 64-bit wall-clock stamps (see brr_session.cpp)
+  SY_WORDS = 224
 };
+
+// Pipeline rings: partial-dot slabs, their arrival counters and reduction counts cycle over
+// NPAR blocks (block s uses s % NPAR); change lists over NSLOT slots (s % NSLOT).  With a lag
+// of L blocks (streamers apply block s-1-L's changes before streaming block s; the solver
+// corrects block s's dots for blocks s-1 .. s-L through cross-Gram blocks) the streamers run
+// at most L blocks ahead of the solver: NPAR >= L + 1, NSLOT >= L + 2.
+constexpr int NPAR = 3;
+constexpr int NSLOT = 4;
+constexpr int LAG_MAX = 2;
 
 // Stats vector (reduced over markers, summed across shards):
 //   [0] sum beta^2  [1] sum beta^2/lambda  [2 .. 2+G) betaAcum[g]  [2+G .. 2+G+G*K) v[g][k]
@@ -90,18 +99,20 @@ struct Dev {
   int *comp, *forder;
   uint8_t *sel;
   double *gram, *xgram, *xgramT;
+  double *xgram2, *xgram2T;  // lag 2: X_b^T X_{b+2 mod nb} and its transpose (else nullptr)
+  int lag;                   // pipeline lag L (1 or 2, see NPAR)
   int *member, *gidx, *bsz, *gblk, *blkorder;
   double *slab1, *slab2;   // [2][RG*B], [2][NGpad*B]
   int *cnt1;                // [2][NG*NC] level-2 arrival counters (k_stream), cumulative
   int *sync;                // SyncWord block
   int sbase;                // blocks published before this sweep (SY_PEND epoch base)
-  int gbase[2];             // blocks of each parity before this sweep (SY_GDONE / cnt1 epochs)
+  int gbase[NPAR];          // blocks of each ring index before this sweep (SY_GDONE / cnt1 epochs)
   int abase;                // persistent streamer arrivals before this sweep (SY_ARRIVE epoch)
   int64_t slab1_stride, slab2_stride, pend_stride;
-  int *pend_idx, *pend_gi;  // [3][B+16]
-  int *pend_pos;            // [3][B+16] visit position of each change within its block
+  int *pend_idx, *pend_gi;  // [NSLOT][B+16]
+  int *pend_pos;            // [NSLOT][B+16] visit position of each change within its block
   double *pend_bo, *pend_bn;
-  int *pend_n;              // [3] padded counts (multiple of 16), then [3] counts before the padding
+  int *pend_n;              // [NSLOT] padded counts (multiple of 16), then [NSLOT] counts before the padding
   double *rslab;
   int *rcnt;
   double *mslab;

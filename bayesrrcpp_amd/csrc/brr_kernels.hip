@@ -894,7 +894,7 @@ __global__ __launch_bounds__(256, 2) void k_stream(Dev d, int s, const double *e
   const int64_t row0 = (int64_t)rg * SROWS + 4 * lane;
   const bool valid = row0 < d.N;
   const int64_t rowc = valid ? row0 : 0;
-  const int par = s & 1;
+  const int par = s % NPAR;
   // block columns first: their loads depend on nothing
   const int *mem = d.member + (int64_t)s * B + cc * CB + w * CW;
   float4 x[CW];
@@ -916,7 +916,7 @@ __global__ __launch_bounds__(256, 2) void k_stream(Dev d, int s, const double *e
     // per wave and entry hammering the same few lines from every workgroup)
     if (w == 0) {
       if (lane == 0) wait_geq(d.sync + SY_PEND, d.sbase + s - 1, d.sync, 1);
-      const int slot = (s - 2) % 3;
+      const int slot = (s - 2) % NSLOT;
       const int np = ld_sc1_int(d.pend_n + slot);
       const int *pidx = d.pend_idx + slot * d.pend_stride;
       const double *pbo = d.pend_bo + slot * d.pend_stride, *pbn = d.pend_bn + slot * d.pend_stride;
@@ -971,7 +971,7 @@ __global__ __launch_bounds__(256, 2) void k_stream(Dev d, int s, const double *e
   const int grp = rg / STREAM_GROUP;
   const int g0 = grp * STREAM_GROUP;
   const int gsz = min(STREAM_GROUP, d.RG - g0);
-  const int use = d.gbase[par] + (s >> 1);  // earlier blocks of this parity (cumulative counters)
+  const int use = d.gbase[par] + s / NPAR;  // earlier blocks of this ring index (cumulative counters)
   if (last_arriver_wt(cnt1 + grp * NC + cc, (use + 1) * gsz, &s_last)) {
     if (t < CB) {
       double v16[STREAM_GROUP];
@@ -1382,7 +1382,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   const int lane = t & 63, wv = t >> 6;
   const int bs = d.bsz[s];
   const int gb = d.gblk[s];
-  const int par = s & 1;
+  const int par = s % NPAR;
   const bool prof = d.sc->prof_on;
   uint64_t tp0 = prof ? wall_clock64() : 0, tp1 = 0, tp2 = 0, tp3 = 0, tw = 0;
   const double sigmaE = d.sc->sigmaE;
@@ -1391,19 +1391,6 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   const bool resident = B <= RESIDENT_BMAX && nslot >= B + solve_scratch_rows(B, NT);
 
   // A) everything that does not depend on k_stream(s)
-  const double *C = nullptr;
-  int np_prev = 0;
-  const int *pv_gi = nullptr;
-  const double *pv_bo = nullptr, *pv_bn = nullptr;
-  if (s > 0) {  // cross-Gram rows of the previous block (cycle neighbours)
-    const int gp = d.gblk[s - 1];
-    C = (gb == (gp + 1) % d.nb) ? d.xgram + (int64_t)gp * B * B : d.xgramT + (int64_t)gb * B * B;
-    const int slot = (s - 1) % 3;
-    np_prev = ld_sc1_int(d.pend_n + slot);  // written with sc1 stores by the previous block
-    pv_gi = d.pend_gi + slot * d.pend_stride;
-    pv_bo = d.pend_bo + slot * d.pend_stride;
-    pv_bn = d.pend_bn + slot * d.pend_stride;
-  }
 #pragma unroll
   for (int c = 0; c < NPT; ++c) {
     const int pos = t + NT * c;
@@ -1431,50 +1418,70 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       }
     }
   }
-  // sum_i (x_j . x_i) delta_i over block s-1's changes.  The change list (padded to a multiple
-  // of 16) is staged in the slot area, which is free until step 2; with B < NT the NT / B
-  // thread groups take contiguous parts of the list and their partial sums are added in group
-  // order.
+  // sum_i (x_j . x_i) delta_i over the changes of the blocks the streamed dots have not seen:
+  // block s-1 (cross-Gram of cycle neighbours), and with lag 2 also block s-2 (cross-Gram of
+  // blocks two apart), added in that order.  Each change list (padded to a multiple of 16) is
+  // staged in the slot area, which is free until step 2; with B < NT the NT / B thread groups
+  // take contiguous parts of a list and their partial sums are added in group order.
   constexpr int PG = B < NT ? NT / B : 1;
   double *scr = resident ? slots + (int64_t)B * B : slots;
   double *Lcd = scr;
   int *Lcg = reinterpret_cast<int *>(scr + (B + 16));
   double *Lpart = scr + (B + 16) + (B + 16) / 2 + 1;
-  for (int e = t; e < np_prev; e += NT) {
-    Lcg[e] = ld_sc1_int(pv_gi + e);
-    Lcd[e] = ld_sc1(pv_bn + e) - ld_sc1(pv_bo + e);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int c = 0; c < NPT; ++c) {
-    const int pos = (t % (B < NT ? B : NT)) + NT * c;
-    const int grp = B < NT ? t / B : 0;
-    const int nch = np_prev / 16;
-    const int c0 = grp * nch / PG, c1 = (grp + 1) * nch / PG;
-    double corr = 0.0;
-    if (pos < bs) {
-      const int gi = Lgi[pos];
-      for (int ch = c0; ch < c1; ++ch) {
-        double cv[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) cv[u] = C[(int64_t)Lcg[16 * ch + u] * B + gi];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) corr += cv[u] * Lcd[16 * ch + u];
+  const int nlist = d.lag == 2 ? 2 : 1;
+  for (int l = 0; l < nlist; ++l) {
+    const int sp = s - 1 - l;  // the earlier block
+    if (l > 0 && sp < 0) break;
+    if (l > 0) __syncthreads();  // every thread is done with the previous list's staging / partials
+    const double *C = nullptr;
+    int np_prev = 0;
+    if (sp >= 0) {
+      const int gp = d.gblk[sp];
+      if (l == 0)
+        C = (gb == (gp + 1) % d.nb) ? d.xgram + (int64_t)gp * B * B : d.xgramT + (int64_t)gb * B * B;
+      else
+        C = (gb == (gp + 2) % d.nb) ? d.xgram2 + (int64_t)gp * B * B : d.xgram2T + (int64_t)gb * B * B;
+      const int slot = sp % NSLOT;
+      np_prev = ld_sc1_int(d.pend_n + slot);  // written with sc1 stores by that block's solve
+      const int *pv_gi = d.pend_gi + slot * d.pend_stride;
+      const double *pv_bo = d.pend_bo + slot * d.pend_stride, *pv_bn = d.pend_bn + slot * d.pend_stride;
+      for (int e = t; e < np_prev; e += NT) {
+        Lcg[e] = ld_sc1_int(pv_gi + e);
+        Lcd[e] = ld_sc1(pv_bn + e) - ld_sc1(pv_bo + e);
       }
     }
-    if (PG == 1) {
-      if (pos < bs) Lr0[pos] = corr;
-    } else {
-      Lpart[grp * B + pos] = corr;
-    }
-  }
-  if (PG > 1) {
     __syncthreads();
-    if (t < bs) {
-      double corr = Lpart[t];
 #pragma unroll
-      for (int g = 1; g < PG; ++g) corr += Lpart[g * B + t];
-      Lr0[t] = corr;
+    for (int c = 0; c < NPT; ++c) {
+      const int pos = (t % (B < NT ? B : NT)) + NT * c;
+      const int grp = B < NT ? t / B : 0;
+      const int nch = np_prev / 16;
+      const int c0 = grp * nch / PG, c1 = (grp + 1) * nch / PG;
+      double corr = 0.0;
+      if (pos < bs) {
+        const int gi = Lgi[pos];
+        for (int ch = c0; ch < c1; ++ch) {
+          double cv[16];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) cv[u] = C[(int64_t)Lcg[16 * ch + u] * B + gi];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) corr += cv[u] * Lcd[16 * ch + u];
+        }
+      }
+      if (PG == 1) {
+        if (pos < bs) Lr0[pos] = l == 0 ? corr : Lr0[pos] + corr;
+      } else {
+        Lpart[grp * B + pos] = corr;
+      }
+    }
+    if (PG > 1) {
+      __syncthreads();
+      if (t < bs) {
+        double corr = Lpart[t];
+#pragma unroll
+        for (int g = 1; g < PG; ++g) corr += Lpart[g * B + t];
+        Lr0[t] = l == 0 ? corr : Lr0[t] + corr;
+      }
     }
   }
   if (resident) {
@@ -1490,7 +1497,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   }
   // B) wait for k_stream(s)'s reduction groups (other queue; cumulative count)
   if (t == 0 && s == 0) stamp(d.sync, 3);
-  if (t == 0) wait_geq(d.sync + SY_GDONE + 32 * par, (d.gbase[par] + (s >> 1) + 1) * d.gtarget, d.sync, 3);
+  if (t == 0) wait_geq(d.sync + SY_GDONE + 32 * par, (d.gbase[par] + s / NPAR + 1) * d.gtarget, d.sync, 3);
   if (t == 0 && s == 0) stamp(d.sync, 4);
   if (resident) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces landed
   __syncthreads();
@@ -1810,7 +1817,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   if (prof) tp3 = wall_clock64();
   const uint64_t tc3 = prof ? __builtin_amdgcn_s_memtime() : 0;
   // 4) write back, compact the changed markers into this block's list (position order)
-  const int pslot = s % 3;
+  const int pslot = s % NSLOT;
   int *pidx = d.pend_idx + pslot * d.pend_stride, *pgi = d.pend_gi + pslot * d.pend_stride;
   int *ppos = d.pend_pos + pslot * d.pend_stride;
   double *pbo = d.pend_bo + pslot * d.pend_stride, *pbn = d.pend_bn + pslot * d.pend_stride;
@@ -1860,7 +1867,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   }
   if (t == 0) {
     st_sc1_int(d.pend_n + pslot, npad);
-    st_sc1_int(d.pend_n + 3 + pslot, npend);
+    st_sc1_int(d.pend_n + NSLOT + pslot, npend);
   }
   // publish: every storing wave drains its sc1 stores, then the block count (k_stream(s+2))
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1954,7 +1961,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
   const float4 lval = lcopy ? lsrc[t] : make_float4(0.f, 0.f, 0.f, 0.f);
   if (t < 64) {
     const int np = ld_sc1_int(d.pend_n + slot);
-    const int nr = ld_sc1_int(d.pend_n + 3 + slot);  // entries before the neutral padding
+    const int nr = ld_sc1_int(d.pend_n + NSLOT + slot);  // entries before the neutral padding
     const int *pidx = d.pend_idx + slot * d.pend_stride;
     const double *pbo = d.pend_bo + slot * d.pend_stride, *pbn = d.pend_bn + slot * d.pend_stride;
     for (int e = lane; e < np; e += 64) {
@@ -2038,9 +2045,13 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   const bool prof = d.sc->prof_on;
   // 2-bit storage: the value tables of blocks s - 2 .. s + 1 in LDS (buffer s & 3): block s + 1's
   // are staged at boundary s (inside the apply), block s - 2's serve the apply
+  const int LAG = d.lag;
+  const int NLB = LAG + 3;  // value-table buffers: blocks s-1-LAG (apply) .. s+1 (staged)
+  const int NCC = LAG + 2;  // code-cache buffers: blocks s-1-LAG (apply) .. s (being streamed)
+  auto lut_of = [&](int s) __attribute__((always_inline)) { return s_lut + (int64_t)(s % NLB) * B; };
   auto stage_lut = [&](int s) __attribute__((always_inline)) {
     if constexpr (XF) {
-      for (int i = t; i < B; i += SWEEP_NT) s_lut[(s & 3) * B + i] = d.xlut_ord[(int64_t)s * B + i];
+      for (int i = t; i < B; i += SWEEP_NT) lut_of(s)[i] = d.xlut_ord[(int64_t)s * B + i];
     }
   };
   for (int i = t; i < npass * SROWS; i += SWEEP_NT) eps_l[i] = r0 + i < r1 ? d.eps[r0 + i] : 0.0;
@@ -2056,7 +2067,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   // 2-bit storage with room in LDS: the code bytes of this workgroup's rows of the last three
   // blocks (buffer s % 3), so the change list of block s - 2 is applied from LDS, not HBM
   auto cache_of = [&](int s) __attribute__((always_inline)) -> const uint8_t * {
-    return (XF && s_codes) ? s_codes + (int64_t)(s % 3) * B * (npass * 64) : nullptr;
+    return (XF && s_codes) ? s_codes + (int64_t)(s % NCC) * B * (npass * 64) : nullptr;
   };
   const int items = NCH * npass; // (chunk, pass) items per wave and block
   const int total = items * nb;
@@ -2103,19 +2114,23 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     const int s = it / items, rem = it - s * items;
     const int c = rem / npass, p = rem - c * npass;
     const bool blk_end = rem == items - 1;
-    if (rem == 0 && s == 1) {
+    if (rem == 0 && s >= 1 && s <= LAG) {
+      // a boundary without a change list to apply yet: stage block s+1's tables / indices
       if constexpr (XF) {
-        if (nb > 2) stage_lut(2);  // (buffer 2: no wave reads it before the barrier)
-      } else if (nb > 2) {
-        __syncthreads();  // every wave is done issuing block 0's items
-        for (int i = t; i < B; i += SWEEP_NT) s_mem[i] = d.member[2 * B + i];
+        if (s + 1 < nb) stage_lut(s + 1);  // (its buffer is not read before the barrier)
+      } else if (s + 1 < nb) {
+        __syncthreads();  // every wave is done issuing block s-1's items (same member buffer)
+        for (int i = t; i < B; i += SWEEP_NT) s_mem[((s + 1) & 1) * B + i] = d.member[(int64_t)(s + 1) * B + i];
       }
       __syncthreads();
     }
-    if (rem == 0 && s >= 2) {
-      // block boundary: bring the residual rows from E_{s-2} to E_{s-1} (block s-2's changes)
+    if (rem == 0 && s >= LAG + 1) {
+      // block boundary: apply block a = s-1-LAG's changes to the residual rows (lag 1: they
+      // then hold every change before block s-1, which the solver corrects for through the
+      // cross-Gram; lag 2: before block s-2, corrected for blocks s-2 and s-1)
+      const int a = s - 1 - LAG;
       if (t == 0 && !BRR_EXP_NO_WAIT) {
-        wait_geq(d.sync + SY_PEND, d.sbase + s - 1, d.sync, 2);
+        wait_geq(d.sync + SY_PEND, d.sbase + a + 1, d.sync, 2);
         if (prof) {
           tr_first(d, s, TR_PEND_FIRST);
           tr_last(d, s, TR_PEND_LAST);
@@ -2125,10 +2140,10 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
         }
       }
       if (!BRR_EXP_NO_APPLY)
-        apply_pending<XF>(d, (s - 2) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np,
+        apply_pending<XF>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np,
                           (!XF && s + 1 < nb) ? d.member + (int64_t)(s + 1) * B : nullptr, s_mem + ((s + 1) & 1) * B,
-                          cache_of(s - 2), s_mem, (XF && s + 1 < nb) ? d.xlut_ord + (int64_t)(s + 1) * B : nullptr,
-                          s_lut + ((s + 1) & 3) * B, s_lut + ((s - 2) & 3) * B);
+                          cache_of(a), s_mem, (XF && s + 1 < nb) ? d.xlut_ord + (int64_t)(s + 1) * B : nullptr,
+                          lut_of(s + 1), lut_of(a));
       if (prof && t == 0) {
         tr_last(d, s, TR_APPLY_LAST);
         if (s == nb / 2) d.trace[(int64_t)nb * 16 + 1024 + g] = wall_clock64();  // per-workgroup probe
@@ -2146,9 +2161,9 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     for (int j = 0; j < CW; ++j) {
       float4 xv;
       if constexpr (XF) {
-        xv = x_decode4(xq[0][j], s_lut[(s & 3) * B + w * CPW + c * CW + j]);
+        xv = x_decode4(xq[0][j], lut_of(s)[w * CPW + c * CW + j]);
         // code cache: block s's bytes at position w CPW + c CW + j, row byte p 64 + lane
-        if (s_codes) s_codes[((s % 3) * B + w * CPW + c * CW + j) * (npass * 64) + p * 64 + lane] = (uint8_t)xq[0][j];
+        if (s_codes) s_codes[((s % NCC) * B + w * CPW + c * CW + j) * (npass * 64) + p * 64 + lane] = (uint8_t)xq[0][j];
       } else {
         xv = xq[0][j];
       }
@@ -2172,7 +2187,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
 #pragma unroll
       for (int j = 0; j < CW; ++j) v[j] = 0.0;
       const int col = w * CPW + c * CW + lcol;
-      if ((lane & (64 / CW - 1)) == 0) st_sc1(d.slab1 + (s & 1) * d.slab1_stride + (int64_t)g * B + col, r);
+      if ((lane & (64 / CW - 1)) == 0) st_sc1(d.slab1 + (s % NPAR) * d.slab1_stride + (int64_t)g * B + col, r);
     }
     if (blk_end) {
       // block done.  The partial-dot stores were issued before the next item's loads, so
@@ -2186,7 +2201,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       // per-wave arrivals measured 1.6x slower, contention on the group counters)
       __syncthreads();
       if (t == 0)
-        __hip_atomic_fetch_add(d.cnt1 + (s & 1) * d.NG + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(d.cnt1 + (s % NPAR) * d.NG + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (t == 0) {
         if (prof) {
           tr_first(d, s, TR_ITEMS_FIRST);
@@ -2205,15 +2220,11 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     acc[1024 + g] = acc_apply;
     acc[2048 + g] = acc_stream;
   }
-  // end of sweep: the last two blocks' changes, then the residual rows back to HBM
+  // end of sweep: the last LAG + 1 blocks' changes, then the residual rows back to HBM
   if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + nb, d.sync, 4);
-  if (nb >= 2)
-    apply_pending<XF>(d, (nb - 2) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, nullptr, nullptr,
-                      cache_of(nb - 2), s_mem, nullptr, nullptr, s_lut + ((nb - 2) & 3) * B);
-  else
-    __syncthreads();
-  apply_pending<XF>(d, (nb - 1) % 3, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, nullptr, nullptr,
-                    cache_of(nb - 1), s_mem, nullptr, nullptr, s_lut + ((nb - 1) & 3) * B);
+  for (int a = max(0, nb - 1 - LAG); a < nb; ++a)
+    apply_pending<XF>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, nullptr, nullptr, cache_of(a),
+                      s_mem, nullptr, nullptr, lut_of(a));
   for (int i = t; i < npass * SROWS; i += SWEEP_NT)
     if (r0 + i < r1) d.eps[r0 + i] = eps_l[i];
 }
@@ -2227,8 +2238,8 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
   const int ng = (nsg + FUSED_GROUP - 1) / FUSED_GROUP;
   const int B = d.B;
   for (int s = 0; s < d.nb; ++s) {
-    const int par = s & 1;
-    const int use = d.gbase[par] + (s >> 1);
+    const int par = s % NPAR;
+    const int use = d.gbase[par] + s / NPAR;
     const double *slab1 = d.slab1 + par * d.slab1_stride;
     for (int grp = r; grp < ng; grp += nred) {
       const int gw0 = grp * FUSED_GROUP, gsz = min(FUSED_GROUP, nsg - gw0);
@@ -2277,7 +2288,7 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
     // being applied, member indices of two blocks (fused_config)
     double *eps_l = reinterpret_cast<double *>(smem);
     float4 *s_lut = reinterpret_cast<float4 *>(eps_l + (int64_t)npass * SROWS);
-    double *s_pbo = reinterpret_cast<double *>(s_lut + (XF ? 4 * d.B : 0)), *s_pbn = s_pbo + (d.B + 16);
+    double *s_pbo = reinterpret_cast<double *>(s_lut + (XF ? (d.lag + 3) * d.B : 0)), *s_pbn = s_pbo + (d.B + 16);
     int *s_pidx = reinterpret_cast<int *>(s_pbn + (d.B + 16));
     int *s_mem = s_pidx + (d.B + 16);  // 16-B aligned: B + 16 is a multiple of 4
     // (2-bit storage: s_mem holds the change positions instead; then the code cache)
@@ -2603,9 +2614,9 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   if ((size_t)nslot * d.B < solve_scratch_doubles(d.B, SWEEP_NT)) return false;
   // streamers: residual rows, [the value tables of two blocks], the change list (indices, old and
   // new betas), the member indices of two blocks in LDS
-  const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double) + (xf ? (size_t)d.B * 64 : 0) +
+  const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double) + (xf ? (size_t)d.B * 16 * (d.lag + 3) : 0) +
                            (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int)) + 2 * sizeof(int) * d.B;
-  const size_t code_bytes = xf ? (size_t)3 * d.B * npass * 64 : 0;
+  const size_t code_bytes = xf ? (size_t)(d.lag + 2) * d.B * npass * 64 : 0;
   const bool ccache = xf && eps_bytes + code_bytes <= budget && !getenv("BRR_NO_CODE_CACHE");
   const size_t lds = std::max(fixed + (size_t)nslot * 8 * d.B, eps_bytes + (ccache ? code_bytes : 0));
   if (lds > budget) return false;

@@ -121,7 +121,7 @@ struct brr_session {
   Dev d{};
   int device = 0;
   hipStream_t st = nullptr;
-  int sbase = 0, gbase[2] = {0, 0}, abase = 0;  // hand-over counter epochs (see SyncWord)
+  int sbase = 0, gbase[NPAR] = {0, 0, 0}, abase = 0;  // hand-over counter epochs (see SyncWord)
   FusedCfg fused;       // fused persistent sweep (nsg == 0: per-block kernels)
   int64_t N = 0, M = 0, M_total = 0, col_offset = 0;
   int K = 1, G = 1, F = 0, B = 128, nb = 0, model = 0, NS = 0;
@@ -273,13 +273,11 @@ int do_sweep_local(brr_session *s) {
     if (int rc = rows_flagged(s, H_ROW_SNAPSHOT)) return rc;
   // epoch bases of the hand-over counters (cumulative over the session)
   d.sbase = s->sbase;
-  d.gbase[0] = s->gbase[0];
-  d.gbase[1] = s->gbase[1];
+  for (int k = 0; k < NPAR; ++k) d.gbase[k] = s->gbase[k];
   d.abase = s->abase;
   if (s->fused.nsg > 0) s->abase += s->fused.nsg + 1 + s->fused.nred;
   s->sbase += s->nb;
-  s->gbase[0] += (s->nb + 1) / 2;
-  s->gbase[1] += s->nb / 2;
+  for (int k = 0; k < NPAR; ++k) s->gbase[k] += (s->nb + NPAR - 1 - k) / NPAR;  // blocks s with s % NPAR == k
   // per-marker constants of the sweep in visit order
   HIPCHK(launch_prep(d, it, s->st));
   // the hot loop (lag-1 pipeline).  Fused: ONE persistent launch, workgroup 0 solves block s
@@ -341,7 +339,7 @@ int do_sweep_local(brr_session *s) {
   // E_{nb-2} (written by the last k_stream) minus the changes of the last two blocks; the
   // fused sweep has already applied them and written eps
   const double *elast = fused ? d.eps : ebuf[s->nb & 1];
-  const int sa = (!fused && s->nb >= 2) ? (s->nb - 2) % 3 : -1, sb = fused ? -1 : (s->nb - 1) % 3;
+  const int sa = (!fused && s->nb >= 2) ? (s->nb - 2) % NSLOT : -1, sb = fused ? -1 : (s->nb - 1) % NSLOT;
   if (sharded) {
     if (!s->ex_eps || !s->ex_stats) { set_error("exchange buffers not set"); return -1; }
     Dev dx = d;
@@ -519,16 +517,16 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   d.slab1_stride = (int64_t)(d.RG + 1) * B;  // per-block: RG row tiles; fused: 2 nsg <= RG + 1 slices
   d.slab2_stride = (int64_t)NGpad * B;
   d.pend_stride = B + 16;
-  rc |= s->alloc(&d.slab1, 2 * d.slab1_stride);
-  rc |= s->alloc(&d.slab2, 2 * d.slab2_stride);
-  rc |= s->alloc(&d.cnt1, 2 * (int64_t)d.NG * NC);
+  rc |= s->alloc(&d.slab1, NPAR * d.slab1_stride);
+  rc |= s->alloc(&d.slab2, NPAR * d.slab2_stride);
+  rc |= s->alloc(&d.cnt1, NPAR * (int64_t)d.NG * NC);
   rc |= s->alloc(&d.sync, SY_WORDS);
-  rc |= s->alloc(&d.pend_idx, 3 * d.pend_stride);
-  rc |= s->alloc(&d.pend_pos, 3 * d.pend_stride);
-  rc |= s->alloc(&d.pend_gi, 3 * d.pend_stride);
-  rc |= s->alloc(&d.pend_bo, 3 * d.pend_stride);
-  rc |= s->alloc(&d.pend_bn, 3 * d.pend_stride);
-  rc |= s->alloc(&d.pend_n, 6);  // [3] padded list lengths, [3] entries before the padding
+  rc |= s->alloc(&d.pend_idx, NSLOT * d.pend_stride);
+  rc |= s->alloc(&d.pend_pos, NSLOT * d.pend_stride);
+  rc |= s->alloc(&d.pend_gi, NSLOT * d.pend_stride);
+  rc |= s->alloc(&d.pend_bo, NSLOT * d.pend_stride);
+  rc |= s->alloc(&d.pend_bn, NSLOT * d.pend_stride);
+  rc |= s->alloc(&d.pend_n, 2 * NSLOT);  // [NSLOT] padded list lengths, [NSLOT] entries before the padding
   rc |= s->alloc(&d.trace, (int64_t)s->nb * 16 + 5120);  // + per-workgroup probes and totals
   d.nbB = (int64_t)s->nb * B;
   rc |= s->alloc(&d.mc, d.nbB * (3 + 2 * std::max(K, 1)));
@@ -543,18 +541,18 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   d.gAssign = nullptr;
   // every buffer a kernel may read before writing is zeroed here (recycled device memory
   // holds the previous session's values): slab2 pad rows, member padding, pending list
-  bool ok = hipMemsetAsync(d.cnt1, 0, sizeof(int) * 2 * d.NG * NC, s->st) == hipSuccess &&
+  bool ok = hipMemsetAsync(d.cnt1, 0, sizeof(int) * NPAR * d.NG * NC, s->st) == hipSuccess &&
             hipMemsetAsync(d.sync, 0, sizeof(int) * SY_WORDS, s->st) == hipSuccess &&
-            hipMemsetAsync(d.pend_gi, 0, sizeof(int) * 3 * d.pend_stride, s->st) == hipSuccess &&
+            hipMemsetAsync(d.pend_gi, 0, sizeof(int) * NSLOT * d.pend_stride, s->st) == hipSuccess &&
             hipMemsetAsync(d.pend_n, 0, sizeof(int) * 6, s->st) == hipSuccess &&
             hipMemsetAsync(d.eps, 0, sizeof(double) * d.ld, s->st) == hipSuccess &&
             hipMemsetAsync(d.eps2, 0, sizeof(double) * d.ld, s->st) == hipSuccess &&
-            hipMemsetAsync(d.slab2, 0, sizeof(double) * 2 * d.slab2_stride, s->st) == hipSuccess &&
+            hipMemsetAsync(d.slab2, 0, sizeof(double) * NPAR * d.slab2_stride, s->st) == hipSuccess &&
             hipMemsetAsync(d.member, 0, sizeof(int) * s->nb * B, s->st) == hipSuccess &&
             hipMemsetAsync(d.gidx, 0, sizeof(int) * s->nb * B, s->st) == hipSuccess &&
-            hipMemsetAsync(d.pend_idx, 0, sizeof(int) * 3 * d.pend_stride, s->st) == hipSuccess &&
-            hipMemsetAsync(d.pend_pos, 0, sizeof(int) * 3 * d.pend_stride, s->st) == hipSuccess &&
-            hipMemsetAsync(d.pend_bo, 0, sizeof(double) * 3 * d.pend_stride, s->st) == hipSuccess &&
+            hipMemsetAsync(d.pend_idx, 0, sizeof(int) * NSLOT * d.pend_stride, s->st) == hipSuccess &&
+            hipMemsetAsync(d.pend_pos, 0, sizeof(int) * NSLOT * d.pend_stride, s->st) == hipSuccess &&
+            hipMemsetAsync(d.pend_bo, 0, sizeof(double) * NSLOT * d.pend_stride, s->st) == hipSuccess &&
             hipMemsetAsync(d.pend_bn, 0, sizeof(double) * 3 * d.pend_stride, s->st) == hipSuccess &&
             hipMemsetAsync(d.rcnt, 0, sizeof(int), s->st) == hipSuccess &&
             hipMemsetAsync(d.mcnt, 0, sizeof(int), s->st) == hipSuccess &&
@@ -579,7 +577,18 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   {
     const char *pb = getenv("BRR_PER_BLOCK");
     const char *cap = getenv("BRR_STREAM_WG");
+    // lag 2 (fused sweep, BLOCKED order, nb >= 4; BRR_LAG=1 keeps lag 1): the streamers apply
+    // block s-3's changes before streaming block s, so a workgroup can run two blocks ahead of
+    // the solver and per-block jitter is absorbed; costs the cross-Gram blocks of blocks two
+    // apart (2 nb B^2 f64 more, computed once at init)
+    const char *lg = getenv("BRR_LAG");
+    d.lag = (s->order_mode == BRR_ORDER_BLOCKED && s->nb >= 4 && !(lg && atoi(lg) == 1)) ? 2 : 1;
     if (!(pb && pb[0] == '1') && !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused)) s->fused = FusedCfg{};
+    if (s->fused.nsg == 0) d.lag = 1;
+    if (d.lag == 2 && (s->alloc(&d.xgram2, (int64_t)s->nb * B * B) || s->alloc(&d.xgram2T, (int64_t)s->nb * B * B))) {
+      delete s;
+      return nullptr;
+    }
   }
   s->ref_order.resize((size_t)M);
   for (int64_t i = 0; i < M; ++i) s->ref_order[(size_t)i] = (int32_t)i;
@@ -920,6 +929,7 @@ int brr_session_init(brr_session *s, int32_t seed) {
   HIPCHK(launch_perm(d, 0, s->shard, true, s->st));
   HIPCHK(launch_gram(d, 0, d.gram, nullptr, s->st));
   HIPCHK(launch_gram(d, 1, d.xgram, d.xgramT, s->st));  // cycle neighbours (b, b+1 mod nb)
+  if (d.lag == 2) HIPCHK(launch_gram(d, 2, d.xgram2, d.xgram2T, s->st));  // (b, b+2 mod nb)
   HIPCHK(launch_xsq(d, s->st));
   Scal sc{};
   if (s->model == MODEL_RESTART) { sc.mu = s->mu0; sc.sigmaE = s->sigmaE0; }

@@ -125,12 +125,12 @@ def test_v2_large_blocks(brr, oracle_mod, require_gpu, B):
         _compare(s, orc, O, L, L.MODEL_V2, tag=f"B={B} it={it}")
 
 
-@pytest.mark.parametrize("mode", ["persistent", "persistent-cap7", "persistent-cap30", "per-block"])
+@pytest.mark.parametrize("mode", ["persistent", "persistent-cap7", "persistent-cap30", "persistent-lag1", "per-block"])
 def test_pipeline_modes_midsize(brr, oracle_mod, require_gpu, monkeypatch, mode):
     """The sweep pipeline at a size with many streaming workgroups and reduction groups: the fused
     persistent sweep (256 rows per streaming workgroup; 7 workgroups of 12 passes; 29 workgroups
-    of 704 rows -- row ranges start on 64-row boundaries -- the last one ragged) and the
-    per-block kernels, all against the oracle over several sweeps."""
+    of 704 rows -- row ranges start on 64-row boundaries -- the last one ragged; lag 2 and lag 1)
+    and the per-block kernels, all against the oracle over several sweeps."""
     from bayesrrcpp_amd import _lib as L
     O = oracle_mod
     cap = {"persistent-cap7": 7, "persistent-cap30": 30}.get(mode)
@@ -138,6 +138,8 @@ def test_pipeline_modes_midsize(brr, oracle_mod, require_gpu, monkeypatch, mode)
         monkeypatch.setenv("BRR_STREAM_WG", str(cap))
     if mode == "per-block":
         monkeypatch.setenv("BRR_PER_BLOCK", "1")
+    if mode == "persistent-lag1":  # the fused sweep with the lag-1 pipeline (default: lag 2)
+        monkeypatch.setenv("BRR_LAG", "1")
     N = 20000
     X, Y, _ = _cohort(O, N, 3000, n_causal=60)
     s, orc = _make(brr, O, L.MODEL_V2, X, Y, 0, B=512)
