@@ -577,12 +577,18 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   {
     const char *pb = getenv("BRR_PER_BLOCK");
     const char *cap = getenv("BRR_STREAM_WG");
-    // lag 2 (fused sweep, BLOCKED order, nb >= 4; BRR_LAG=1 keeps lag 1): the streamers apply
-    // block s-3's changes before streaming block s, so a workgroup can run two blocks ahead of
-    // the solver and per-block jitter is absorbed; costs the cross-Gram blocks of blocks two
-    // apart (2 nb B^2 f64 more, computed once at init)
+    // lag 2 (fused sweep, BLOCKED order, nb >= 4): the streamers apply block s-3's changes
+    // before streaming block s, so a workgroup can run two blocks ahead of the solver and
+    // per-block jitter among the streamers is absorbed; costs the cross-Gram blocks of blocks
+    // two apart (2 nb B^2 f64 more, computed once at init) and a second correction in the
+    // solver.  Chosen where the streamers bound the sweep: f32 storage and the samplers that
+    // change few markers per block (V2, restart; C2 26.3 -> 27.2 sweeps/s); the solver-bound
+    // Groups / Horseshoe chains and the 2-bit storage keep lag 1 (lag 2 measured 9 / 25 / 7 %
+    // slower there).  BRR_LAG=1|2 overrides.
     const char *lg = getenv("BRR_LAG");
-    d.lag = (s->order_mode == BRR_ORDER_BLOCKED && s->nb >= 4 && !(lg && atoi(lg) == 1)) ? 2 : 1;
+    const bool lag2_ok = s->order_mode == BRR_ORDER_BLOCKED && s->nb >= 4;
+    const bool lag2_pref = !s->x2bit && (model == MODEL_V2 || model == MODEL_RESTART);
+    d.lag = (lag2_ok && (lg ? atoi(lg) == 2 : lag2_pref)) ? 2 : 1;
     if (!(pb && pb[0] == '1') && !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused)) s->fused = FusedCfg{};
     if (s->fused.nsg == 0) d.lag = 1;
     if (d.lag == 2 && (s->alloc(&d.xgram2, (int64_t)s->nb * B * B) || s->alloc(&d.xgram2T, (int64_t)s->nb * B * B))) {

@@ -363,3 +363,35 @@ def test_recycled_device_memory(brr, oracle_mod, require_gpu):
         _compare(s, orc, O, L, L.MODEL_V2, tag=f"recycled N={N} B={B}")
         del s, orc
         gc.collect()
+
+
+@pytest.mark.parametrize("lag", [1, 2])
+@pytest.mark.parametrize("model", [1, 2, 3])  # Groups, restart, Horseshoe
+def test_pipeline_lag_all_models(brr, oracle_mod, require_gpu, monkeypatch, model, lag):
+    """Both pipeline lags for the models whose default is the other one (V2: lag 2, Groups and
+    Horseshoe: lag 1), against the oracle: many blocks, several streaming workgroups."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    monkeypatch.setenv("BRR_LAG", str(lag))
+    monkeypatch.setenv("BRR_STREAM_WG", "5")
+    N, P = 1500, 1100
+    X, Y, _ = _cohort(O, N, P, n_causal=30)
+    kw = {}
+    if model == L.MODEL_GROUPS:
+        G = 3
+        kw = dict(G=G, gAssign=(np.arange(P) * G // P).astype(np.int32),
+                  fixed=np.linspace(-1, 1, N).reshape(N, 1))
+    elif model == L.MODEL_RESTART:
+        rng = np.random.default_rng(3)
+        comp0 = rng.integers(0, 4, P).astype(np.float64)
+        beta0 = np.where(comp0 > 0, rng.normal(0, 0.02, P), 0.0)
+        kw = dict(restart=dict(mu0=0.01, beta0=beta0, sigmaE0=0.7, sigmaGG0=np.array([0.3]),
+                               eps0=Y - X @ beta0 - 0.01, comp0=comp0))
+    elif model == L.MODEL_HORSESHOE:
+        kw = dict(hs=dict(A=0.01, v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0))
+    s, orc = _make(brr, O, model, X, Y, 0, B=128, **kw)
+    assert s.scalar(104) > 1  # fused sweep
+    for it in range(4):
+        s.sweep(1)
+        orc.sweep(1)
+        _compare(s, orc, O, L, model, tag=f"model={model} lag={lag} it={it}")
