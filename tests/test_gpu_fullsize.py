@@ -42,8 +42,9 @@ def test_c2_residual_invariant(brr, oracle_mod, require_gpu):
     assert err < 1e-9, err
 
 
-def test_c2_2bit_chain_identical(brr, require_gpu):
+def test_c2_2bit_chain_identical(brr, require_gpu, monkeypatch):
     from bayesrrcpp_amd import _lib as L
+    monkeypatch.setenv("BRR_LAG", "2")  # both storages on the f32 default pipeline (lag 2)
     traj = []
     s = _c2_session(brr, L, L.X_F32)
     for _ in range(4):

@@ -13,6 +13,13 @@ from conftest import CVA, HYP
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _same_lag(monkeypatch):
+    # the automatic pipeline lag differs between the storages (f32 V2: 2, 2-bit: 1) and the two
+    # lags order the floating-point corrections differently: compare the storages at one lag
+    monkeypatch.setenv("BRR_LAG", "1")
+
 RTOL = 1e-9
 
 
