@@ -1094,6 +1094,7 @@ int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
     case 102: *out = (double)sc.prof_on; return 0;
     case 104: *out = (double)s->fused.nsg; return 0;  // fused sweep: streaming workgroups (0 = per-block)
     case 105: *out = (double)s->fused.ccache; return 0;  // fused sweep: 2-bit code cache in LDS
+    case 106: *out = (double)s->d.lag; return 0;  // pipeline lag
     case 110: case 111: case 112: case 113: case 114: case 115: case 116: case 117: case 118: case 119:
     case 120: case 121:
       *out = (double)sc.prof[which - 110]; return 0;

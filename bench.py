@@ -380,7 +380,7 @@ def main():
                      + ("2-bit codes + f32 value tables" if x2 else "f32 X") + ", f64 arithmetic)"),
             "config": {"workload": cfg["workload"] + (" [2-bit genotype storage, SURVEY 8f3]" if x2 else ""),
                        "x_storage": args.x_storage, "N": N, "P": P, "K": K, "groups": G,
-                       "block_size": Bsz, "order": "blocked", "fused_stream_wg": int(s.scalar(104)), "code_cache": int(s.scalar(105)), "parallelism": f"column-shard x{world}",
+                       "block_size": Bsz, "order": "blocked", "fused_stream_wg": int(s.scalar(104)), "code_cache": int(s.scalar(105)), "pipeline_lag": int(s.scalar(106)), "parallelism": f"column-shard x{world}",
                        "setup_s": round(t_setup, 2), "diag": diag},
             "roofline": roof, "cpu_baseline": cpu,
         }
