@@ -48,9 +48,9 @@ CONFIGS = {
 }
 
 
-def block_events(raw):
+def block_events(raw, lag=1):
     """Medians over the blocks of one traced sweep.  'lat_*' are measured from the solver's
-    publication of block s-2's changes, which is what streaming block s waits for."""
+    publication of block s-1-lag's changes, which is what streaming block s waits for."""
     import numpy as np
     raw = np.asarray(raw, dtype=np.float64)
     nbk = (raw.size - 5120) // 16
@@ -63,7 +63,7 @@ def block_events(raw):
     if nb < 6:
         return {}
     sl = slice(4, nb - 1)
-    pub_m2 = np.roll(tr[:, 3], 2)
+    pub_m2 = np.roll(tr[:, 3], lag + 1)
     ev = {
         "period": np.diff(tr[:, 0])[sl],
         "solver_wait": (tr[:, 1] - tr[:, 0])[sl],
@@ -366,7 +366,7 @@ def main():
             # per-block event trace of one fused sweep (brr_kernels.hip TR_*), medians in us
             s.set_scalar(102, 1.0)
             s.sweep(1)
-            diag["block_events_us"] = block_events(s.vector(201))
+            diag["block_events_us"] = block_events(s.vector(201), int(s.scalar(106)))
         s.set_scalar(102, 0.0)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
