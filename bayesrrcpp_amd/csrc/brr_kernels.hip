@@ -1924,14 +1924,6 @@ constexpr int SWEEP_NW = SWEEP_NT / 64;
 #ifndef STREAM_P2
 #define STREAM_P2 3   // the same for 2-bit codes (a byte per column and lane; vmcnt <= 63 caps P CW)
 #endif
-// timing experiments only (results are wrong with either set): skip the streamers' wait for the
-// change list, or the apply of the list
-#ifndef BRR_EXP_NO_WAIT
-#define BRR_EXP_NO_WAIT 0
-#endif
-#ifndef BRR_EXP_NO_APPLY
-#define BRR_EXP_NO_APPLY 0
-#endif
 constexpr int FUSED_GROUP = 16;  // streaming workgroups (slab rows) per level-2 reduction group
 
 // Block `slot`'s change list applied to this workgroup's residual rows:
@@ -2129,7 +2121,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       // then hold every change before block s-1, which the solver corrects for through the
       // cross-Gram; lag 2: before block s-2, corrected for blocks s-2 and s-1)
       const int a = s - 1 - LAG;
-      if (t == 0 && !BRR_EXP_NO_WAIT) {
+      if (t == 0) {
         wait_geq(d.sync + SY_PEND, d.sbase + a + 1, d.sync, 2);
         if (prof) {
           tr_first(d, s, TR_PEND_FIRST);
@@ -2139,8 +2131,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
           t_mark = tn;
         }
       }
-      if (!BRR_EXP_NO_APPLY)
-        apply_pending<XF>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np,
+      apply_pending<XF>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np,
                           (!XF && s + 1 < nb) ? d.member + (int64_t)(s + 1) * B : nullptr, s_mem + ((s + 1) & 1) * B,
                           cache_of(a), s_mem, (XF && s + 1 < nb) ? d.xlut_ord + (int64_t)(s + 1) * B : nullptr,
                           lut_of(s + 1), lut_of(a));
