@@ -2132,9 +2132,9 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
         }
       }
       apply_pending<XF>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np,
-                          (!XF && s + 1 < nb) ? d.member + (int64_t)(s + 1) * B : nullptr, s_mem + ((s + 1) & 1) * B,
-                          cache_of(a), s_mem, (XF && s + 1 < nb) ? d.xlut_ord + (int64_t)(s + 1) * B : nullptr,
-                          lut_of(s + 1), lut_of(a));
+                        (!XF && s + 1 < nb) ? d.member + (int64_t)(s + 1) * B : nullptr, s_mem + ((s + 1) & 1) * B,
+                        cache_of(a), s_mem, (XF && s + 1 < nb) ? d.xlut_ord + (int64_t)(s + 1) * B : nullptr,
+                        lut_of(s + 1), lut_of(a));
       if (prof && t == 0) {
         tr_last(d, s, TR_APPLY_LAST);
         if (s == nb / 2) d.trace[(int64_t)nb * 16 + 1024 + g] = wall_clock64();  // per-workgroup probe
