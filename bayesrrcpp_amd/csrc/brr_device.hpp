@@ -59,10 +59,10 @@ struct Hyper {
 enum SyncWord : int {
   SY_PEND = 0,     // blocks whose k_solve has published its change list (session total)
   SY_GDONE = 32,   // + 32 * (s % NPAR): level-2 reduction groups completed (session total)
-  SY_ERR = 128,    // a bounded wait expired; SY_ERR + 1..4: site, target, value seen, workgroup
-  SY_ARRIVE = 160, // persistent streamer workgroups that started (session total)
-  SY_TS = 192,     // diagnostics: 64-bit wall-clock stamps (see brr_session.cpp)
-  SY_WORDS = 224
+  SY_ERR = 160,    // a bounded wait expired; SY_ERR + 1..4: site, target, value seen, workgroup
+  SY_ARRIVE = 192, // persistent streamer workgroups that started (session total)
+  SY_TS = 224,     // diagnostics: 64-bit wall-clock stamps (see brr_session.cpp)
+  SY_WORDS = 256
 };
 
 // Pipeline rings: partial-dot slabs, their arrival counters and reduction counts cycle over
@@ -70,9 +70,9 @@ enum SyncWord : int {
 // of L blocks (streamers apply block s-1-L's changes before streaming block s; the solver
 // corrects block s's dots for blocks s-1 .. s-L through cross-Gram blocks) the streamers run
 // at most L blocks ahead of the solver: NPAR >= L + 1, NSLOT >= L + 2.
-constexpr int NPAR = 3;
-constexpr int NSLOT = 4;
-constexpr int LAG_MAX = 2;
+constexpr int NPAR = 4;
+constexpr int NSLOT = 5;
+constexpr int LAG_MAX = 3;
 
 // Stats vector (reduced over markers, summed across shards):
 //   [0] sum beta^2  [1] sum beta^2/lambda  [2 .. 2+G) betaAcum[g]  [2+G .. 2+G+G*K) v[g][k]
@@ -99,7 +99,8 @@ struct Dev {
   int *comp, *forder;
   uint8_t *sel;
   double *gram, *xgram, *xgramT;
-  double *xgram2, *xgram2T;  // lag 2: X_b^T X_{b+2 mod nb} and its transpose (else nullptr)
+  double *xgram2, *xgram2T;  // lag >= 2: X_b^T X_{b+2 mod nb} and its transpose (else nullptr)
+  double *xgram3, *xgram3T;  // lag 3: X_b^T X_{b+3 mod nb} and its transpose (else nullptr)
   int lag;                   // pipeline lag L (1 or 2, see NPAR)
   int *member, *gidx, *bsz, *gblk, *blkorder;
   double *slab1, *slab2;   // [2][RG*B], [2][NGpad*B]

@@ -1428,7 +1428,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   double *Lcd = scr;
   int *Lcg = reinterpret_cast<int *>(scr + (B + 16));
   double *Lpart = scr + (B + 16) + (B + 16) / 2 + 1;
-  const int nlist = d.lag == 2 ? 2 : 1;
+  const int nlist = d.lag;
   for (int l = 0; l < nlist; ++l) {
     const int sp = s - 1 - l;  // the earlier block
     if (l > 0 && sp < 0) break;
@@ -1439,8 +1439,10 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       const int gp = d.gblk[sp];
       if (l == 0)
         C = (gb == (gp + 1) % d.nb) ? d.xgram + (int64_t)gp * B * B : d.xgramT + (int64_t)gb * B * B;
-      else
+      else if (l == 1)
         C = (gb == (gp + 2) % d.nb) ? d.xgram2 + (int64_t)gp * B * B : d.xgram2T + (int64_t)gb * B * B;
+      else
+        C = (gb == (gp + 3) % d.nb) ? d.xgram3 + (int64_t)gp * B * B : d.xgram3T + (int64_t)gb * B * B;
       const int slot = sp % NSLOT;
       np_prev = ld_sc1_int(d.pend_n + slot);  // written with sc1 stores by that block's solve
       const int *pv_gi = d.pend_gi + slot * d.pend_stride;

@@ -121,7 +121,7 @@ struct brr_session {
   Dev d{};
   int device = 0;
   hipStream_t st = nullptr;
-  int sbase = 0, gbase[NPAR] = {0, 0, 0}, abase = 0;  // hand-over counter epochs (see SyncWord)
+  int sbase = 0, gbase[NPAR] = {}, abase = 0;  // hand-over counter epochs (see SyncWord)
   FusedCfg fused;       // fused persistent sweep (nsg == 0: per-block kernels)
   int64_t N = 0, M = 0, M_total = 0, col_offset = 0;
   int K = 1, G = 1, F = 0, B = 128, nb = 0, model = 0, NS = 0;
@@ -588,10 +588,12 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     const char *lg = getenv("BRR_LAG");
     const bool lag2_ok = s->order_mode == BRR_ORDER_BLOCKED && s->nb >= 4;
     const bool lag2_pref = !s->x2bit && (model == MODEL_V2 || model == MODEL_RESTART);
-    d.lag = (lag2_ok && (lg ? atoi(lg) == 2 : lag2_pref)) ? 2 : 1;
+    d.lag = (lag2_ok && (lg ? atoi(lg) >= 2 : lag2_pref)) ? 2 : 1;
+    if (d.lag == 2 && lg && atoi(lg) >= 3 && s->nb >= 5) d.lag = 3;  // (diagnostics: BRR_LAG=3)
     if (!(pb && pb[0] == '1') && !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused)) s->fused = FusedCfg{};
     if (s->fused.nsg == 0) d.lag = 1;
-    if (d.lag == 2 && (s->alloc(&d.xgram2, (int64_t)s->nb * B * B) || s->alloc(&d.xgram2T, (int64_t)s->nb * B * B))) {
+    if ((d.lag >= 2 && (s->alloc(&d.xgram2, (int64_t)s->nb * B * B) || s->alloc(&d.xgram2T, (int64_t)s->nb * B * B))) ||
+        (d.lag >= 3 && (s->alloc(&d.xgram3, (int64_t)s->nb * B * B) || s->alloc(&d.xgram3T, (int64_t)s->nb * B * B)))) {
       delete s;
       return nullptr;
     }
@@ -935,7 +937,8 @@ int brr_session_init(brr_session *s, int32_t seed) {
   HIPCHK(launch_perm(d, 0, s->shard, true, s->st));
   HIPCHK(launch_gram(d, 0, d.gram, nullptr, s->st));
   HIPCHK(launch_gram(d, 1, d.xgram, d.xgramT, s->st));  // cycle neighbours (b, b+1 mod nb)
-  if (d.lag == 2) HIPCHK(launch_gram(d, 2, d.xgram2, d.xgram2T, s->st));  // (b, b+2 mod nb)
+  if (d.lag >= 2) HIPCHK(launch_gram(d, 2, d.xgram2, d.xgram2T, s->st));  // (b, b+2 mod nb)
+  if (d.lag >= 3) HIPCHK(launch_gram(d, 3, d.xgram3, d.xgram3T, s->st));  // (b, b+3 mod nb)
   HIPCHK(launch_xsq(d, s->st));
   Scal sc{};
   if (s->model == MODEL_RESTART) { sc.mu = s->mu0; sc.sigmaE = s->sigmaE0; }

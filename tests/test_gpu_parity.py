@@ -365,11 +365,11 @@ def test_recycled_device_memory(brr, oracle_mod, require_gpu):
         gc.collect()
 
 
-@pytest.mark.parametrize("lag", [1, 2])
+@pytest.mark.parametrize("lag", [1, 2, 3])
 @pytest.mark.parametrize("model", [1, 2, 3])  # Groups, restart, Horseshoe
 def test_pipeline_lag_all_models(brr, oracle_mod, require_gpu, monkeypatch, model, lag):
-    """Both pipeline lags for the models whose default is the other one (V2: lag 2, Groups and
-    Horseshoe: lag 1), against the oracle: many blocks, several streaming workgroups."""
+    """Every pipeline lag (default: 2 for V2 / restart on f32, 1 otherwise; 3 is opt-in) for the
+    other models, against the oracle: many blocks, several streaming workgroups."""
     from bayesrrcpp_amd import _lib as L
     O = oracle_mod
     monkeypatch.setenv("BRR_LAG", str(lag))
