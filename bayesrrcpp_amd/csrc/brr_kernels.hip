@@ -1926,7 +1926,13 @@ constexpr int SWEEP_NW = SWEEP_NT / 64;
 #ifndef STREAM_P2
 #define STREAM_P2 3   // the same for 2-bit codes (a byte per column and lane; vmcnt <= 63 caps P CW)
 #endif
-constexpr int FUSED_GROUP = 16;  // streaming workgroups (slab rows) per level-2 reduction group
+// streaming workgroups (slab rows) per level-2 reduction group: 64 -> 4 reducer workgroups at C2
+// (16 / 32 / 64 measured 27.1 / 27.6 / 28.1 sweeps/s: fewer reducers, fewer slab2 rows for the
+// solver to sum; 64 doubles per reducer thread is the register limit of the unrolled sum)
+#ifndef FUSED_GROUP_N
+#define FUSED_GROUP_N 64
+#endif
+constexpr int FUSED_GROUP = FUSED_GROUP_N;
 
 // Block `slot`'s change list applied to this workgroup's residual rows:
 // eps_i += x_ij b_old - x_ij b_new in list order (BayesRv2.cpp:191,243).  The rows are cut into
