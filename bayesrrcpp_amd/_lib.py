@@ -49,7 +49,7 @@ EXPORTED = [
     "brr_session_sweep_finish", "brr_session_get_scalar", "brr_session_get_vector",
     "brr_session_set_vector", "brr_session_set_scalar", "brr_session_iteration",
     "brr_session_set_timing", "brr_session_timing", "brr_session_block_size",
-    "brr_session_synchronize",
+    "brr_session_synchronize", "brr_session_linear_predictor",
 ]
 
 _lib = None
@@ -124,6 +124,7 @@ def lib():
     L.brr_session_block_size.restype = C.c_int64
     L.brr_session_block_size.argtypes = [vp]
     L.brr_session_synchronize.argtypes = [vp]
+    L.brr_session_linear_predictor.argtypes = [vp, D]
     _lib = L
     return L
 

@@ -2470,6 +2470,22 @@ __global__ void k_hyper_init(Dev d, const double *stats, int pi_given) {
   }
 }
 
+// Linear predictor X beta + F alpha of this shard (validation read-back, not on the sweep path):
+// one thread per row, columns in index order, f64 accumulation of the stored f32 values.  A plain
+// kernel sharing nothing with the sweep's streaming code, so the full-size residual invariant
+// eps = Y - mu - X beta - F alpha checks the sweep's bookkeeping against an independent product.
+__global__ __launch_bounds__(256) void k_linpred(Dev d, double *out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= d.N) return;
+  double acc = 0.0;
+  for (int64_t j = 0; j < d.M; ++j) {
+    const double b = d.beta[j];
+    if (b != 0.0) acc = __builtin_fma((double)x_at(d, j, i), b, acc);
+  }
+  for (int c = 0; c < d.F; ++c) acc = __builtin_fma(d.fixed[(int64_t)c * d.N + i], d.alpha[c], acc);
+  out[i] = acc;
+}
+
 }  // namespace brr
 
 // ======================================================================================
@@ -2706,6 +2722,11 @@ hipError_t set_solve_lds_limit(int /*B*/) {
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+hipError_t launch_linpred(const Dev &d, double *out, hipStream_t st) {
+  hipLaunchKernelGGL(k_linpred, dim3(cdiv64(d.N, 256)), dim3(256), 0, st, d, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_markers(const Dev &d, int mode, uint32_t it, hipStream_t st) {

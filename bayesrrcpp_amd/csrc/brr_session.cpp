@@ -1223,6 +1223,21 @@ int brr_session_set_vector(brr_session *s, int32_t which, const double *in) {
   return rc;
 }
 
+int brr_session_linear_predictor(brr_session *s, double *out) {
+  if (!s || !out) { set_error("linear_predictor: null argument"); return -1; }
+  if (!s->have_x) { set_error("linear_predictor: X not uploaded"); return -1; }
+  double *tmp = nullptr;
+  if (int rc = dalloc(&tmp, s->N)) return rc;
+  int rc = 0;
+  if (launch_linpred(s->d, tmp, s->st) != hipSuccess || hipStreamSynchronize(s->st) != hipSuccess ||
+      hipMemcpy(out, tmp, sizeof(double) * (size_t)s->N, hipMemcpyDeviceToHost) != hipSuccess) {
+    set_error("linear_predictor: %s", hipGetErrorString(hipGetLastError()));
+    rc = -2;
+  }
+  (void)hipFree(tmp);
+  return rc;
+}
+
 int32_t brr_session_iteration(brr_session *s) { return s ? s->iteration : -1; }
 
 int brr_session_set_timing(brr_session *s, int32_t on) {

@@ -184,6 +184,12 @@ class Session:
                 raise L.BrrError(f"get_vector({which}): {L.last_error()}")
         return out
 
+    def linear_predictor(self):
+        """X beta + F alpha of this shard (N doubles; plain validation kernel, not the sweep path)."""
+        out = np.zeros(self.N)
+        L.check(L.lib().brr_session_linear_predictor(self.h, _d(out)), "linear_predictor")
+        return out
+
     def set_vector(self, which, arr):
         arr = np.ascontiguousarray(arr, dtype=np.float64)
         L.check(L.lib().brr_session_set_vector(self.h, which, _d(arr)), "set_vector")

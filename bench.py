@@ -105,7 +105,9 @@ def block_events(raw, lag=1):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one process each).  Without WORLD_SIZE in the environment, N > 1 spawns the N "
+                         "rank processes itself; with WORLD_SIZE set (torch.distributed.run) it must equal N")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10,
                     help="untimed sweeps (burn-in: the first sweeps from beta = 0 change ~25%% of markers)")
@@ -183,6 +185,18 @@ def pmc_traffic(args, N, P, B, fused, x_bytes):
     return None, None
 
 
+def host_cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(args, P_full):
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--config", args.config,
            "--cpu-markers", str(args.cpu_markers), "--cpu-sweeps", str(args.cpu_sweeps),
@@ -200,6 +214,7 @@ def cpu_baseline(args, P_full):
         "unit": "sweeps/s (extrapolated: 1 / (P x t_marker))",
         "cores": 1,
         "kind": "port",
+        "host_cpu": host_cpu_model(), "host_nproc": os.cpu_count(),
         "sample": (f"CPU oracle (reference-faithful C restatement, f64, y~ materialised, 1 thread "
                    f"pinned) N={r['N']} x {r['markers']} markers, {args.cpu_sweeps} sweeps; "
                    f"t_marker={t_marker * 1e3:.4f} ms; P={P_full}"),
@@ -208,12 +223,43 @@ def cpu_baseline(args, P_full):
 
 
 # ------------------------------------------------------------------------------------------
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """--gpus N without a launcher: start N fresh rank processes of this script (one per GPU,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on 127.0.0.1) and exit with the worst
+    return code.  This parent never touches the GPU, so nothing is exec'd from a GPU process."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def main():
     args = parse()
     if args.cpu_baseline_child:
         cpu_baseline_child(args)
         return
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus is not None and args.gpus > 1:
+            sys.exit(spawn_ranks(args.gpus))
+        world = 1
+    else:
+        world = int(env_world)
+        if args.gpus is not None and args.gpus != world:
+            sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to time a mislabelled run")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None

@@ -186,6 +186,10 @@ int64_t brr_session_get_vector(brr_session *s, int32_t which, double *out /* may
 int brr_session_set_vector(brr_session *s, int32_t which, const double *in);
 int brr_session_set_scalar(brr_session *s, int32_t which, double v);
 int32_t brr_session_iteration(brr_session *s);
+/* validation read-back: out[i] = sum_j X[i,j] beta_j + sum_c fixed[i,c] alpha_c over this shard's
+ * markers (N doubles), computed by a plain row kernel independent of the sweep kernels; used by
+ * the full-size residual invariant eps = Y - mu - X beta - F alpha */
+int brr_session_linear_predictor(brr_session *s, double *out /* N */);
 
 /* instrumentation: per-launch HIP-event timing of the streaming kernel (dots + residual
  * update), accumulated over the sweeps run while enabled. */

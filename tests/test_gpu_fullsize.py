@@ -58,3 +58,78 @@ def test_c2_2bit_chain_identical(brr, require_gpu, monkeypatch):
         assert np.array_equal(s.vector(L.COMP), c), f"comp differs at sweep {it}"
         assert np.array_equal(s.vector(L.EPS), e), f"eps differs at sweep {it}"
         assert s.scalar(L.SIGMAE) == se and s.scalar(L.MU) == mu, f"scalars differ at sweep {it}"
+
+
+def test_linear_predictor_small(brr, oracle_mod, require_gpu):
+    """The validation product X beta + F alpha (used by the full-size invariants below) against numpy."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    n, p, G = 777, 300, 3
+    X, Y, _ = O.synth_cohort(DS, n, p, h2=0.5, n_causal=20)
+    rng = np.random.default_rng(5)
+    fixed = rng.normal(size=(n, 2))
+    for xs in (L.X_F32, L.X_2BIT):
+        s = brr.Session(L.MODEL_GROUPS, n, p, K=4, groups=G, F=2, x_storage=xs)
+        s.upload_x(X).set_y(Y).set_fixed(fixed)
+        s.set_bayesr(**HYP, cva=np.tile(CVA, (G, 1)), gAssign=(np.arange(p) % G).astype(np.int32))
+        s.init(1)
+        beta = np.where(rng.random(p) < 0.4, rng.normal(size=p), 0.0)
+        alpha = rng.normal(size=2)
+        s.set_vector(L.BETA, beta)
+        s.set_vector(L.ALPHA, alpha)
+        ref = X.astype(np.float64) @ beta + fixed @ alpha
+        got = s.linear_predictor()
+        assert np.max(np.abs(got - ref)) / np.max(np.abs(ref)) < 1e-12
+        s.close()
+
+
+def _invariant(s, L, Y):
+    eps, mu = s.vector(L.EPS), s.scalar(L.MU)
+    ref = Y - mu - s.linear_predictor()
+    return float(np.max(np.abs(eps - ref)) / np.max(np.abs(ref)))
+
+
+def test_c3_residual_invariant(brr, require_gpu):
+    """C3 (BayesRSamplerV2Groups, 22 groups, gAssign = floor(22 j / P), one all-zero fixed column,
+    vignettes/BayesRR.Rmd:166) at full size: after 10 sweeps eps = Y - mu - X beta - F alpha
+    (BayesRv2Groups.cpp:203,212-214,220-224,243,295) within 1e-9; sigmaGG finite and positive, every
+    group's pi a probability vector, v counts add up to P."""
+    from bayesrrcpp_amd import _lib as L
+    G = 22
+    s = brr.Session(L.MODEL_GROUPS, N, P, K=4, groups=G, F=1)
+    s.synthesize(DS, 0.5, -1)
+    s.set_bayesr(**HYP, cva=np.tile(CVA, (G, 1)), gAssign=(np.arange(P) * G // P).astype(np.int32))
+    s.set_fixed(np.zeros((N, 1)))
+    s.init(1)
+    Y = s.vector(L.EPS).copy()  # eps after init = Y - mu with mu = 0 (BayesRv2Groups.cpp:203)
+    s.sweep(10)
+    err = _invariant(s, L, Y)
+    sgg, pi, vc = s.vector(L.SIGMAGG), s.vector(L.PI).reshape(G, 4), s.vector(L.VCOUNT)
+    nz = int(np.count_nonzero(s.vector(L.BETA)))
+    s.close()
+    assert err < 1e-9, err
+    assert np.all(np.isfinite(sgg)) and np.all(sgg > 0)
+    assert np.all(pi >= 0) and np.allclose(pi.sum(1), 1.0, rtol=1e-12)
+    assert vc.sum() == P and 0 < nz <= P
+
+
+def test_c4_residual_invariant(brr, require_gpu):
+    """C4 (HorseshoeR, A = (1/sqrt N) 1500 / (P - 1500), HorseshoeR.cpp:315-323) at full size: after
+    10 sweeps eps = Y - mu - X beta (HorseshoeR.cpp:186,210-212,224,238) within 1e-9; every marker moved
+    (Horseshoe resamples all); lambda, tau, c2, eta finite and positive (HorseshoeR.cpp:242-253)."""
+    from bayesrrcpp_amd import _lib as L
+    s = brr.Session(L.MODEL_HORSESHOE, N, P, K=1)
+    s.synthesize(DS, 0.5, -1)
+    s.set_horseshoe(A=(1 / N ** 0.5) * 1500 / (P - 1500), v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0, c2=1.0,
+                    vC=10.0, sC=10.0)
+    s.init(1)
+    Y = s.vector(L.EPS).copy()  # eps after init = Y - mu - X 0 (HorseshoeR.cpp:186)
+    s.sweep(10)
+    err = _invariant(s, L, Y)
+    lam, beta = s.vector(L.LAMBDA), s.vector(L.BETA)
+    sc = [s.scalar(w) for w in (L.TAU, L.C2, L.ETA, L.SIGMAE)]
+    s.close()
+    assert err < 1e-9, err
+    assert np.count_nonzero(beta) == P
+    assert np.all(np.isfinite(lam)) and np.all(lam > 0)
+    assert all(np.isfinite(v) and v > 0 for v in sc), sc

@@ -395,3 +395,136 @@ def test_pipeline_lag_all_models(brr, oracle_mod, require_gpu, monkeypatch, mode
         s.sweep(1)
         orc.sweep(1)
         _compare(s, orc, O, L, model, tag=f"model={model} lag={lag} it={it}")
+
+
+@pytest.mark.parametrize("lag", [1, 2])
+def test_groups_22_c3_layout(brr, oracle_mod, require_gpu, monkeypatch, lag):
+    """C3's group layout at a size the oracle runs in seconds: G = 22, gAssign = floor(22 j / P),
+    identical cva rows, one all-zero fixed column (vignettes/BayesRR.Rmd:166); B = 128 (the
+    automatic Groups block), several streaming workgroups (BayesRv2Groups.cpp:216-312)."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    monkeypatch.setenv("BRR_LAG", str(lag))
+    N, P, G = 3000, 4400, 22
+    X, Y, _ = _cohort(O, N, P, n_causal=60)
+    gA = (np.arange(P) * G // P).astype(np.int32)
+    s, orc = _make(brr, O, L.MODEL_GROUPS, X, Y, 0, B=128, G=G, gAssign=gA, fixed=np.zeros((N, 1)))
+    assert s.scalar(104) > 1  # fused sweep
+    for it in range(5):
+        s.sweep(1)
+        orc.sweep(1)
+        _compare(s, orc, O, L, L.MODEL_GROUPS, tag=f"G=22 lag={lag} it={it}")
+        assert _rel(s.vector(L.BETAACUM), orc.vector(O.V_BETAACUM)) < RTOL
+        assert _rel([s.scalar(L.SIGMAF)], [orc.scalar(O.S_SIGMAF)]) < RTOL
+    assert s.vector(L.SIGMAGG).size == G and len(set(s.vector(L.SIGMAGG))) == G
+
+
+def _csv_rows(path):
+    lines = open(path).read().splitlines()
+    return lines
+
+
+def _compare_csv(p_gpu, p_orc, header=True):
+    g, o = _csv_rows(p_gpu), _csv_rows(p_orc)
+    assert len(g) == len(o) and len(g) > int(header)
+    if header:
+        assert g[0] == o[0]
+    for lg, lo in zip(g[int(header):], o[int(header):]):
+        a = np.array([float(v) for v in lg.split(", ")])
+        b = np.array([float(v) for v in lo.split(", ")])
+        assert a.shape == b.shape
+        assert np.allclose(a, b, rtol=2e-5, atol=1e-9)  # 6 significant digits on both sides
+
+
+def test_oneshot_csv_groups(brr, oracle_mod, require_gpu, tmp_path):
+    """brr_BayesRSamplerV2Groups writes the reference's Groups CSV (header and rows,
+    BayesRv2Groups.cpp:25-54,314-318) equal to the oracle's."""
+    O = oracle_mod
+    N, P, G = 150, 260, 3
+    X, Y, _ = _cohort(O, N, P, n_causal=15)
+    gA = (np.arange(P) % G).astype(np.int32)
+    cva = np.tile(CVA, (G, 1))
+    fixed = np.linspace(-1, 1, 2 * N).reshape(N, 2)
+    pg, po = str(tmp_path / "g.csv"), str(tmp_path / "o.csv")
+    brr.BayesRSamplerV2Groups(pg, 4, 24, 8, 3, X, Y, HYP["sigma0"], HYP["v0E"], HYP["s02E"], HYP["v0G"],
+                              HYP["s02G"], cva, G, gA, fixed, block_size=128, log=lambda m: None)
+    O.run_csv(po, O.GROUPS, X, Y, 24, 8, 3, cva=cva, G=G, gAssign=gA, fixed=fixed, seed=4, order_mode=0,
+              block_size=128, **HYP)
+    _compare_csv(pg, po)
+    assert open(pg).readline().rstrip("\n").endswith("alpha[1],alpha[2],sigmaF")
+
+
+def test_oneshot_csv_restart(brr, oracle_mod, require_gpu, tmp_path):
+    """brr_BRV2Grstart: no header (BRv2Grstart.cpp:26 unused), rows as the reference's sample
+    (BRv2Grstart.cpp:262-268), equal to the oracle's."""
+    O = oracle_mod
+    N, P, G = 140, 200, 2
+    X, Y, _ = _cohort(O, N, P, n_causal=12)
+    gA = (np.arange(P) % G).astype(np.int32)
+    cva = np.tile(CVA, (G, 1))
+    rng = np.random.default_rng(8)
+    comp0 = rng.integers(0, 4, P).astype(np.float64)
+    beta0 = np.where(comp0 > 0, rng.normal(0, 0.02, P), 0.0)
+    eps0 = Y - X @ beta0 - 0.02
+    pg, po = str(tmp_path / "g.csv"), str(tmp_path / "o.csv")
+    brr.BRV2Grstart(pg, 6, 20, 5, 2, 0.02, beta0, 0.8, np.array([0.3, 0.2]), X, eps0, comp0, HYP["sigma0"],
+                    HYP["v0E"], HYP["s02E"], HYP["v0G"], HYP["s02G"], cva, G, gA, block_size=512, log=lambda m: None)
+    O.run_csv(po, O.RESTART, X, None, 20, 5, 2, cva=cva, G=G, gAssign=gA, seed=6, order_mode=0, block_size=512,
+              mu0=0.02, beta0=beta0, sigmaE0=0.8, sigmaGG0=np.array([0.3, 0.2]), eps0=eps0, comp0=comp0, N=N, **HYP)
+    _compare_csv(pg, po, header=False)
+    first = open(pg).readline()
+    assert not first.startswith("iteration") and len(first.split(", ")) == 2 + 2 * P + 1 + G + N
+
+
+def test_oneshot_csv_horseshoe(brr, oracle_mod, require_gpu, tmp_path):
+    """brr_HorseshoeR: header with the trailing comma (HorseshoeR.cpp:279-291) and every kept
+    sample (2M+N+3 values plus the uninitialised last slot, HorseshoeR.cpp:157,258), equal to the
+    oracle's."""
+    O = oracle_mod
+    N, P = 160, 240
+    X, Y, _ = _cohort(O, N, P, n_causal=12)
+    hs = dict(A=(1 / np.sqrt(N)) * 24 / (P - 24), v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0)
+    pg, po = str(tmp_path / "g.csv"), str(tmp_path / "o.csv")
+    brr.HorseshoeR(pg, 2, 18, 6, 4, X, Y, hs["A"], hs["v0E"], hs["s02E"], hs["vL"], hs["vT"], hs["c2"], hs["vC"],
+                   hs["sC"], block_size=128, log=lambda m: None)
+    O.run_csv(po, O.HORSESHOE, X, Y, 18, 6, 4, seed=2, order_mode=0, block_size=128, **hs)
+    _compare_csv(pg, po)
+    assert open(pg).readline().rstrip("\n").endswith(f"epsilon[{N}],")
+
+
+def test_f64_x_not_f32_representable(brr, oracle_mod, require_gpu):
+    """The drop-in upload rounds the reference's f64 X to f32 on the device.
+    On an X that is not f32-representable (scale()d dosages plus a 1e-4 jitter), the GPU chain
+    equals the oracle run on the f32-rounded X (rtol 1e-9), and one sweep from the same state
+    deviates from the oracle on the exact f64 X by at most rtol 1e-5 (the rounding of X,
+    2^-24 relative, propagated through one sweep)."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P = 300, 400
+    X, Y, _ = _cohort(O, N, P, n_causal=20)
+    X64 = X.astype(np.float64) + 1e-4 * np.sin(np.arange(N * P, dtype=np.float64)).reshape(N, P)
+    assert not np.array_equal(X64.astype(np.float32).astype(np.float64), X64)
+    X32 = X64.astype(np.float32).astype(np.float64)
+    s, orc32 = _make(brr, O, L.MODEL_V2, X64, Y, 0, B=128)  # session uploads f64 -> f32
+    for it in range(3):
+        s.sweep(1)
+        orc32.sweep(1)
+    orc32b = O.Oracle(O.V2, X32, Y, cva=CVA, seed=7, order_mode=0, block_size=128, **HYP)
+    orc32b.sweep(3)
+    _compare(s, orc32b, O, L, L.MODEL_V2, tag="f64 X vs oracle on f32(X)")
+    # one sweep from the GPU's state, oracle on the exact f64 X
+    o64 = O.Oracle(O.V2, X64, Y, cva=CVA, seed=7, order_mode=0, block_size=128, **HYP)
+    o64.sweep(3)
+    st = dict(beta=s.vector(L.BETA), comp=s.vector(L.COMP), pi=s.vector(L.PI), sigmaE=s.scalar(L.SIGMAE),
+              sigmaG=s.scalar(L.SIGMAG), mu=s.scalar(L.MU))
+    eps64 = Y - st["mu"] - X64 @ st["beta"]
+    o64.set_vector(O.V_BETA, st["beta"]); o64.set_vector(O.V_COMP, st["comp"]); o64.set_vector(O.V_PI, st["pi"])
+    o64.set_vector(O.V_EPS, eps64)
+    o64.set_scalar(O.S_SIGMAE, st["sigmaE"]); o64.set_scalar(O.S_SIGMAG, st["sigmaG"]); o64.set_scalar(O.S_MU, st["mu"])
+    s.sweep(1)
+    o64.sweep(1)
+    same = s.vector(L.COMP) == o64.vector(O.V_COMP)
+    assert same.mean() > 0.99
+    if same.all():
+        assert _rel(s.vector(L.BETA), o64.vector(O.V_BETA)) < 1e-5
+        assert _rel([s.scalar(L.SIGMAE)], [o64.scalar(O.S_SIGMAE)]) < 1e-5
