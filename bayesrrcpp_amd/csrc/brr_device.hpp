@@ -44,7 +44,7 @@ struct Scal {
   unsigned long long n_changed;  // diagnostics: markers whose beta changed
   int prof_on;                   // diagnostics: k_solve phase timers on
   int pad2;
-  unsigned long long prof[12];   // k_solve phase totals (wall_clock64 ticks, 100 MHz), counters
+  unsigned long long prof[16];   // k_solve phase totals (wall_clock64 ticks, 100 MHz), counters
 };
 
 struct Hyper {

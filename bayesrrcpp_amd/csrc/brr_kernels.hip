@@ -27,6 +27,7 @@
 
 #include "brr_device.hpp"
 #include "brr_rng.hpp"
+#include "brr_chain.hpp"
 
 namespace brr {
 
@@ -1363,8 +1364,10 @@ __device__ __forceinline__ void chain_bayesr_resident(const Dev &d, int bs, doub
   }
 }
 
+// persistent: one workgroup solves every block of the sweep in order (LDS persists between blocks)
 template <bool HS, int B, int NT>
-__device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, int nslot, char *smem) {
+__device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, int nslot, char *smem,
+                                            bool persistent) {
 #pragma clang fp contract(off)
   constexpr int NPT = (B + NT - 1) / NT;  // positions per thread, parallel phases
   constexpr int NW = NT / 64;             // waves
@@ -1389,8 +1392,22 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   const int64_t S = d.nbB;
   const int64_t q0 = (int64_t)s * B;
   const bool resident = B <= RESIDENT_BMAX && nslot >= B + solve_scratch_rows(B, NT);
+  // misc[10] / misc[11]: padded length / block of the change list this workgroup left in LDS
+  if (t == 0 && s == 0) misc[11] = -2;
 
-  // A) everything that does not depend on k_stream(s)
+  // A) everything that does not depend on k_stream(s).  Resident mode first starts the LDS-DMA of
+  // block s's whole Gram block (the previous block's copy is no longer read: its chain and write-
+  // back are done) so it lands while the constants and the cross-Gram correction are loaded.
+  if (resident) {
+    // row gi at slots + gi B, 1 KiB per wave-instruction; retired by each wave's vmcnt(0) and the
+    // barrier after it (before the coefficients / decisions read it)
+    constexpr int NCHUNK = B * B * 8 / 1024;
+    const char *src = reinterpret_cast<const char *>(d.gram + (int64_t)gb * B * B);
+    char *dst = reinterpret_cast<char *>(slots);
+    for (int c = wv; c < NCHUNK; c += NW)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + c * 1024 + lane * 16),
+                                       (__attribute__((address_space(3))) void *)(dst + c * 1024), 16, 0, 0);
+  }
 #pragma unroll
   for (int c = 0; c < NPT; ++c) {
     const int pos = t + NT * c;
@@ -1443,13 +1460,19 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
         C = (gb == (gp + 2) % d.nb) ? d.xgram2 + (int64_t)gp * B * B : d.xgram2T + (int64_t)gb * B * B;
       else
         C = (gb == (gp + 3) % d.nb) ? d.xgram3 + (int64_t)gp * B * B : d.xgram3T + (int64_t)gb * B * B;
-      const int slot = sp % NSLOT;
-      np_prev = ld_sc1_int(d.pend_n + slot);  // written with sc1 stores by that block's solve
-      const int *pv_gi = d.pend_gi + slot * d.pend_stride;
-      const double *pv_bo = d.pend_bo + slot * d.pend_stride, *pv_bn = d.pend_bn + slot * d.pend_stride;
-      for (int e = t; e < np_prev; e += NT) {
-        Lcg[e] = ld_sc1_int(pv_gi + e);
-        Lcd[e] = ld_sc1(pv_bn + e) - ld_sc1(pv_bo + e);
+      if (persistent && resident && l == 0 && s >= 1 && misc[11] == s - 1) {
+        // this workgroup wrote block s-1's list into Lcg / Lcd itself (step 4 of that block,
+        // persistent solver): no global round trip
+        np_prev = misc[10];
+      } else {
+        const int slot = sp % NSLOT;
+        np_prev = ld_sc1_int(d.pend_n + slot);  // written with sc1 stores by that block's solve
+        const int *pv_gi = d.pend_gi + slot * d.pend_stride;
+        const double *pv_bo = d.pend_bo + slot * d.pend_stride, *pv_bn = d.pend_bn + slot * d.pend_stride;
+        for (int e = t; e < np_prev; e += NT) {
+          Lcg[e] = ld_sc1_int(pv_gi + e);
+          Lcd[e] = ld_sc1(pv_bn + e) - ld_sc1(pv_bo + e);
+        }
       }
     }
     __syncthreads();
@@ -1462,12 +1485,22 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       double corr = 0.0;
       if (pos < bs) {
         const int gi = Lgi[pos];
-        for (int ch = c0; ch < c1; ++ch) {
-          double cv[16];
+        // two chunks (32 loads) in flight, added in list order
+        for (int ch = c0; ch < c1; ch += 2) {
+          const bool two = ch + 1 < c1;
+          double cv[32];
 #pragma unroll
           for (int u = 0; u < 16; ++u) cv[u] = C[(int64_t)Lcg[16 * ch + u] * B + gi];
+          if (two) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) cv[16 + u] = C[(int64_t)Lcg[16 * ch + 16 + u] * B + gi];
+          }
 #pragma unroll
           for (int u = 0; u < 16; ++u) corr += cv[u] * Lcd[16 * ch + u];
+          if (two) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) corr += cv[16 + u] * Lcd[16 * ch + 16 + u];
+          }
         }
       }
       if (PG == 1) {
@@ -1486,16 +1519,22 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       }
     }
   }
-  if (resident) {
-    // the whole Gram block into the slot area (row gi at slots + gi B) by LDS-DMA, 1 KiB per
-    // wave-instruction; issued after phase A's own loads were consumed, so the copy is in
-    // flight during the wait below and retired by the barrier that follows it
-    constexpr int NCHUNK = B * B * 8 / 1024;
-    const char *src = reinterpret_cast<const char *>(d.gram + (int64_t)gb * B * B);
-    char *dst = reinterpret_cast<char *>(slots);
-    for (int c = wv; c < NCHUNK; c += NW)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + c * 1024 + lane * 16),
-                                       (__attribute__((address_space(3))) void *)(dst + c * 1024), 16, 0, 0);
+  if constexpr (HS) {
+    if (resident) {
+      // the chain's coefficients (G_ij / D_j for i before j, else 0) made in place from the
+      // resident Gram before the wait for the streaming side (D is a per-sweep constant of the
+      // Horseshoe, HorseshoeR.cpp:226-232); the scratch behind the rows holds RN(1/D) and the
+      // position of every Gram index
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces landed
+      __syncthreads();  // (also: the correction's partial sums in the scratch are consumed)
+      double *Linv = scr;
+      int *Lposg = reinterpret_cast<int *>(scr + B);
+      for (int g = t; g < B; g += NT) { Linv[g] = 0.0; Lposg[g] = B; }
+      __syncthreads();
+      for (int pos = t; pos < bs; pos += NT) { Linv[Lgi[pos]] = 1.0 / La[pos]; Lposg[Lgi[pos]] = pos; }
+      __syncthreads();
+      chain_coefficients<B, NT>(slots, Linv, Lposg);
+    }
   }
   // B) wait for k_stream(s)'s reduction groups (other queue; cumulative count)
   if (t == 0 && s == 0) stamp(d.sync, 3);
@@ -1602,8 +1641,12 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   if (resident) {
     if (t < 64) {
       if constexpr (HS) {
-        chain_hs_resident<B>(bs, Lr0, Ldsel, Lsdz, Lbo, Lbn, Lgi, slots);
-        if (prof && lane == 0) atomicAdd(&d.sc->prof[6], (unsigned long long)bs);
+        const uint64_t tq0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+        chain_hs_blocked<B>(bs, Lr0, Ldsel, Lsdz, Lbo, Lbn, Lgi, slots);
+        if (prof && lane == 0) {
+          atomicAdd(&d.sc->prof[6], (unsigned long long)bs);
+          atomicAdd(&d.sc->prof[12], (unsigned long long)(__builtin_amdgcn_s_memtime() - tq0));  // chain loop, shader clocks
+        }
       } else {
         chain_bayesr_resident<B>(d, bs, sigmaE, Lr0, Llo, Lhi, Ldsel, Lsdz, Lbo, Lbn, Lfl, Lks, Lgi, La, Lden, Lp,
                                  Lx2, Lz, Lm, slots, prof);
@@ -1854,12 +1897,20 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       st_sc1_int(ppos + idx, pos);
       st_sc1(pbo + idx, bov);
       st_sc1(pbn + idx, bnv);
+      if (resident) {  // the next block's cross-Gram correction reads it from LDS (phase A)
+        Lcg[idx] = Lgi[pos];
+        Lcd[idx] = bnv - bov;
+      }
     }
     for (int w = 0; w < NW; ++w) base += misc[w];
     __syncthreads();
   }
   const int npend = base;
   const int npad = (npend + 15) & ~15;  // lists are read in batches of 8 / 16
+  if (resident) {
+    if (npend + t < npad) { Lcg[npend + t] = 0; Lcd[npend + t] = 0.0; }
+    if (t == 0) { misc[10] = npad; misc[11] = s; }
+  }
   if (npend + t < npad) {  // neutral padding: eps + x*0 - x*0 == eps exactly, delta = 0
     st_sc1_int(pidx + npend + t, 0);
     st_sc1_int(pgi + npend + t, 0);
@@ -1896,7 +1947,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
 template <bool HS, int B>
 __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it, int nslot) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  solve_block<HS, B, 256>(d, s, it, nslot, smem);
+  solve_block<HS, B, 256>(d, s, it, nslot, smem, false);
 }
 
 
@@ -1934,31 +1985,40 @@ constexpr int SWEEP_NW = SWEEP_NT / 64;
 #endif
 constexpr int FUSED_GROUP = FUSED_GROUP_N;
 
-// Block `slot`'s change list applied to this workgroup's residual rows:
-// eps_i += x_ij b_old - x_ij b_new in list order (BayesRv2.cpp:191,243).  The rows are cut into
-// 64-row slices, one row per lane, spread over the 8 waves; each wave keeps two batches of 16
-// column loads in flight (the list is padded to a multiple of 16 with neutral entries).
+// Block `slot`'s change list applied to this workgroup's residual rows (BayesRv2.cpp:191,243):
+//     eps_i += sum_c x_ic (b_old_c - b_new_c)
+// Lane = 4 consecutive rows (one 16-B load per column, as the stream reads them; 2-bit storage:
+// one code byte), so a wave-instruction covers a 256-row pass.  The 8 waves split the passes,
+// and when there are fewer than 8 passes also the list: wave w takes pass w % npass and the
+// contiguous part w / npass of G = 8 / npass parts of the list (npass >= 8: every wave takes
+// whole passes with the whole list).  Each wave keeps two batches of AB column loads in flight
+// and sums its part in list order; the parts are added to eps in part order through LDS
+// (s_part), so the result does not depend on timing.  (Round 1 loaded one 4-B value per lane
+// and column, 16 in flight: the apply of a 128-change list took 11-18 us of HBM latency.)
 // msrc != nullptr: also copy the B member indices at msrc to mdst (LDS); loaded before the first
-// barrier, stored after it (the buffer's previous block is then no longer read by any wave).
+// barrier, stored after the last (the buffer's previous block is then no longer read by any wave).
 // ccode != nullptr (2-bit storage): the code bytes of the block being applied are in LDS
 // (stream_role's code cache, ccode[pos * npass * 64 + row / 4]); s_ppos receives the positions.
 // 2-bit storage: lsrc / ldst stage the next block's value tables the same way; lutb = the value
-// tables of the block being applied (LDS, by visit position, s_ppos receives the positions).
+// tables of the block being applied (LDS, by visit position).
 template <int XF>
 __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0, int64_t r1, int npass,
                                               double *eps_l, int *s_pidx, double *s_pbo, double *s_pbn,
-                                              int *s_np, const int *msrc = nullptr, int *mdst = nullptr,
-                                              const uint8_t *ccode = nullptr, int *s_ppos = nullptr,
-                                              const float4 *lsrc = nullptr, float4 *ldst = nullptr,
-                                              const float4 *lutb = nullptr) {
+                                              int *s_np, double *s_part, const int *msrc = nullptr,
+                                              int *mdst = nullptr, const uint8_t *ccode = nullptr,
+                                              int *s_ppos = nullptr, const float4 *lsrc = nullptr,
+                                              float4 *ldst = nullptr, const float4 *lutb = nullptr) {
 #pragma clang fp contract(off)
-  constexpr int AB = 16;  // columns per batch
+  constexpr int AB = 4;  // columns per batch (two batches in flight: 8 KiB per wave, 32 VGPRs, as many as the
+                         // streaming ring leaves without spills)
   const int t = threadIdx.x, lane = t & 63;
-  const int w = t >> 6;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const bool mcopy = msrc != nullptr && t < d.B;
   const int mval = mcopy ? msrc[t] : 0;
   const bool lcopy = XF && lsrc != nullptr && t < d.B;
   const float4 lval = lcopy ? lsrc[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+  double *s_pd = s_pbo;  // b_old - b_new per list entry
+  (void)s_pbn;
   if (t < 64) {
     const int np = ld_sc1_int(d.pend_n + slot);
     const int nr = ld_sc1_int(d.pend_n + NSLOT + slot);  // entries before the neutral padding
@@ -1970,58 +2030,93 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
       const int es = e < nr ? e : max(nr - 1, 0);
       s_pidx[e] = ld_sc1_int(pidx + es);
       if (XF) s_ppos[e] = ld_sc1_int(d.pend_pos + slot * d.pend_stride + es);
-      s_pbo[e] = ld_sc1(pbo + e);
-      s_pbn[e] = ld_sc1(pbn + e);
+      s_pd[e] = ld_sc1(pbo + e) - ld_sc1(pbn + e);
     }
     if (lane == 0) s_np[0] = np;
   }
   __syncthreads();
   const int np = __builtin_amdgcn_readfirstlane(s_np[0]);
-  const int64_t ld = d.ld;
-  for (int sl = w; sl < npass * 4; sl += SWEEP_NW) {
-    const int off = sl * 64 + lane;
-    const bool ok = r0 + off < r1;  // rows beyond r1 read row r0 (unconditional loads) and are not stored
-    const int64_t rr = ok ? r0 + off : r0;
-    const float *Xr = XF ? nullptr : d.X + rr;
-    const int cb = npass * 64;  // code bytes per column in the cache
-    auto xload = [&](int e) __attribute__((always_inline)) -> float {
-      const int col = s_pidx[e];
-      if constexpr (XF) {
-        const int pos = s_ppos[e];
-        const uint32_t byte = ccode ? (uint32_t)ccode[pos * cb + (off >> 2)] : (uint32_t)d.Xc[col * d.ldc + (rr >> 2)];
-        return x_sel(lutb[pos], byte >> (2 * ((ccode ? off : rr) & 3)));
-      }
-      else return Xr[(int64_t)col * ld];
-    };
-    double e = eps_l[off];
-    float xa[AB], xb[AB];
-    if (np > 0) {
+  const int G = npass >= SWEEP_NW ? 1 : SWEEP_NW / npass;  // parts of the list
+  const int ldp = npass * SROWS;                          // doubles per part in s_part
+  if (np > 0) {
+    const int p0 = G == 1 ? w : w % npass, part = G == 1 ? 0 : w / npass;
+    const int pstep = G == 1 ? SWEEP_NW : npass;  // (G > 1: one pass per wave)
+    const int e0 = part < G ? (np * part / G) : np, e1 = part < G ? (np * (part + 1) / G) : np;
+    for (int p = p0; p < npass && e0 < e1; p += pstep) {
+      const int off = p * SROWS + 4 * lane;  // this lane's 4 rows, relative to r0
+      const bool ok = r0 + off < r1;
+      const int64_t src = ok ? r0 + off : r0;  // lanes past the rows re-read row r0 (not stored)
+      auto xload = [&](int e) __attribute__((always_inline)) -> float4 {
+        if constexpr (XF) {
+          const int pos = s_ppos[e];
+          const uint32_t byte = ccode ? (uint32_t)ccode[pos * (npass * 64) + (off >> 2)]
+                                      : (uint32_t)d.Xc[(int64_t)s_pidx[e] * d.ldc + (src >> 2)];
+          return x_decode4(byte, lutb[pos]);
+        } else {
+          return ldg4(d.X + (int64_t)s_pidx[e] * d.ld + src);
+        }
+      };
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      float4 xa[AB], xb[AB];
+      auto consume = [&](const float4 (&x)[AB], int e) __attribute__((always_inline)) {
 #pragma unroll
-      for (int q = 0; q < AB; ++q) xa[q] = xload(q);
+        for (int q = 0; q < AB; ++q) {
+          if (e + q < e1) {
+            const double dd = s_pd[e + q];
+            a0 += (double)x[q].x * dd;
+            a1 += (double)x[q].y * dd;
+            a2 += (double)x[q].z * dd;
+            a3 += (double)x[q].w * dd;
+          }
+        }
+      };
+#pragma unroll
+      for (int q = 0; q < AB; ++q) xa[q] = xload(min(e0 + q, e1 - 1));
+      for (int e = e0; e < e1; e += 2 * AB) {
+        const bool more = e + AB < e1;
+        if (more) {
+#pragma unroll
+          for (int q = 0; q < AB; ++q) xb[q] = xload(min(e + AB + q, e1 - 1));
+        }
+        consume(xa, e);
+        if (!more) break;
+        if (e + 2 * AB < e1) {
+#pragma unroll
+          for (int q = 0; q < AB; ++q) xa[q] = xload(min(e + 2 * AB + q, e1 - 1));
+        }
+        consume(xb, e + AB);
+      }
+      if (G == 1) {
+        if (ok) {
+          double *ep = eps_l + off;
+          ep[0] = ep[0] + a0;
+          ep[1] = ep[1] + a1;
+          ep[2] = ep[2] + a2;
+          ep[3] = ep[3] + a3;
+        }
+      } else {
+        double *pp = s_part + (int64_t)part * ldp + off;
+        pp[0] = a0;
+        pp[1] = a1;
+        pp[2] = a2;
+        pp[3] = a3;
+      }
     }
-    for (int p0 = 0; p0 < np; p0 += 2 * AB) {
-      const bool more = p0 + AB < np;
-      if (more) {
-#pragma unroll
-        for (int q = 0; q < AB; ++q) xb[q] = xload(p0 + AB + q);
+    if (G > 1) {
+      // parts without a pass (G npass < 8 waves, or an empty part) hold nothing: zero them first
+      for (int i = t; i < G * ldp; i += SWEEP_NT) {
+        const int part = i / ldp;
+        if (np * part / G == np * (part + 1) / G) s_part[i] = 0.0;
       }
-#pragma unroll
-      for (int q = 0; q < AB; ++q) {
-        const double a = xa[q];
-        e = (e + a * s_pbo[p0 + q]) - a * s_pbn[p0 + q];
-      }
-      if (!more) break;
-      if (p0 + 2 * AB < np) {
-#pragma unroll
-        for (int q = 0; q < AB; ++q) xa[q] = xload(p0 + 2 * AB + q);
-      }
-#pragma unroll
-      for (int q = 0; q < AB; ++q) {
-        const double a = xb[q];
-        e = (e + a * s_pbo[p0 + AB + q]) - a * s_pbn[p0 + AB + q];
+      __syncthreads();
+      for (int i = t; i < ldp; i += SWEEP_NT) {
+        if (r0 + i < r1) {
+          double acc = s_part[i];
+          for (int part = 1; part < G; ++part) acc += s_part[part * ldp + i];
+          eps_l[i] = eps_l[i] + acc;
+        }
       }
     }
-    if (ok) eps_l[off] = e;
   }
   if (mcopy) mdst[t] = mval;
   if (lcopy) ldst[t] = lval;
@@ -2035,7 +2130,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
 template <int CW, int P, int XF>
 __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int npass, double *eps_l, int *s_pidx,
                                             double *s_pbo, double *s_pbn, int *s_np, float4 *s_lut, int *s_mem,
-                                            uint8_t *s_codes) {
+                                            double *s_part, uint8_t *s_codes) {
 #pragma clang fp contract(off)
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -2139,7 +2234,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
           t_mark = tn;
         }
       }
-      apply_pending<XF>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np,
+      apply_pending<XF>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, s_part,
                         (!XF && s + 1 < nb) ? d.member + (int64_t)(s + 1) * B : nullptr, s_mem + ((s + 1) & 1) * B,
                         cache_of(a), s_mem, (XF && s + 1 < nb) ? d.xlut_ord + (int64_t)(s + 1) * B : nullptr,
                         lut_of(s + 1), lut_of(a));
@@ -2222,7 +2317,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   // end of sweep: the last LAG + 1 blocks' changes, then the residual rows back to HBM
   if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + nb, d.sync, 4);
   for (int a = max(0, nb - 1 - LAG); a < nb; ++a)
-    apply_pending<XF>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, nullptr, nullptr, cache_of(a),
+    apply_pending<XF>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, s_part, nullptr, nullptr, cache_of(a),
                       s_mem, nullptr, nullptr, lut_of(a));
   for (int i = t; i < npass * SROWS; i += SWEEP_NT)
     if (r0 + i < r1) d.eps[r0 + i] = eps_l[i];
@@ -2262,7 +2357,7 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
 template <bool HS, int B>
 __device__ __forceinline__ void solver_role(const Dev &d, uint32_t it, int nslot, char *smem) {
   for (int s = 0; s < d.nb; ++s) {
-    solve_block<HS, B, SWEEP_NT>(d, s, it, nslot, smem);
+    solve_block<HS, B, SWEEP_NT>(d, s, it, nslot, smem, true);
     __syncthreads();
   }
 }
@@ -2290,10 +2385,12 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
     double *s_pbo = reinterpret_cast<double *>(s_lut + (XF ? (d.lag + 3) * d.B : 0)), *s_pbn = s_pbo + (d.B + 16);
     int *s_pidx = reinterpret_cast<int *>(s_pbn + (d.B + 16));
     int *s_mem = s_pidx + (d.B + 16);  // 16-B aligned: B + 16 is a multiple of 4
-    // (2-bit storage: s_mem holds the change positions instead; then the code cache)
-    uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_mem + 2 * d.B) : nullptr;
+    // (2-bit storage: s_mem holds the change positions instead); the apply's partial sums; then
+    // the code cache
+    double *s_part = reinterpret_cast<double *>(s_mem + 2 * d.B);
+    uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_part + SWEEP_NW * SROWS) : nullptr;
     stream_role<STREAM_CW, XF ? STREAM_P2 : STREAM_P, XF>(d, (int)blockIdx.x - 1, rpw, npass, eps_l, s_pidx, s_pbo,
-                                                         s_pbn, s_np, s_lut, s_mem, s_codes);
+                                                         s_pbn, s_np, s_lut, s_mem, s_part, s_codes);
   }
 }
 
@@ -2630,7 +2727,8 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   // streamers: residual rows, [the value tables of two blocks], the change list (indices, old and
   // new betas), the member indices of two blocks in LDS
   const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double) + (xf ? (size_t)d.B * 16 * (d.lag + 3) : 0) +
-                           (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int)) + 2 * sizeof(int) * d.B;
+                           (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int)) + 2 * sizeof(int) * d.B +
+                           (size_t)SWEEP_NW * SROWS * sizeof(double);
   const size_t code_bytes = xf ? (size_t)(d.lag + 2) * d.B * npass * 64 : 0;
   const bool ccache = xf && eps_bytes + code_bytes <= budget && !getenv("BRR_NO_CODE_CACHE");
   const size_t lds = std::max(fixed + (size_t)nslot * 8 * d.B, eps_bytes + (ccache ? code_bytes : 0));

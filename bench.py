@@ -408,6 +408,8 @@ def main():
         diag["solve_wait_us"] = round(s.scalar(120) / calls / 100.0, 3)
         # shader clock during the chain: s_memtime ticks / s_memrealtime (100 MHz) ticks
         diag["solve_chain_clock_ghz"] = round(s.scalar(121) / max(1.0, s.scalar(112)) * 0.1, 3)
+        # serial chain loop alone (shader clocks per chain step; wave 0 of the solver)
+        diag["solve_chain_loop_cycles_per_step"] = round(s.scalar(122) / max(1.0, s.scalar(116)), 1)
         if int(s.scalar(104)) > 0:
             # per-block event trace of one fused sweep (brr_kernels.hip TR_*), medians in us
             s.set_scalar(102, 1.0)

@@ -1,0 +1,78 @@
+"""Distributional checks on the CPU oracle (the GPU chain equals the oracle's chain within 1e-9,
+tests/test_gpu_parity.py), in the reference's own spirit: its demo blocks compare posterior
+summaries by eye (src/BayesRv2.cpp:297-331, src/HorseshoeR.cpp:304-347).
+
+1. Visit order: the BLOCKED scan (rotated block cycle + shuffled blocks, the device fast path) and
+   the reference's std::random_shuffle order (BayesRv2.cpp:182) sample the same posterior -- the
+   posterior means of sigmaE, sigmaG, the large effects and the number of non-zero markers agree
+   within 4 Monte-Carlo standard errors (batch means).
+2. Column shards: the 2-shard chain (stale residual of the other shard within a
+   sweep, one exchange per sweep) against the 1-shard chain.  This is NOT exact Gibbs, and at
+   this small, strongly correlated size the bias is measurable: sigmaE's posterior mean comes out
+   1.7 % higher (4.4 Monte-Carlo SE); the test bounds every summary by max(4 SE, 3 %) and
+   records the sigmaE shift.  The exact multi-GPU alternative is the row-sharded protocol
+   (DESIGN.md section 12).
+Fixed seeds: deterministic, not flaky.
+"""
+import numpy as np
+import pytest
+
+from conftest import CVA, HYP
+
+N, P, NC = 400, 240, 8
+BURN, KEEP = 300, 3000
+
+
+def _chain(O, X, Y, seed, **kw):
+    o = O.Oracle(O.V2, X, Y, cva=CVA, seed=seed, **HYP, **kw)
+    o.sweep(BURN)
+    rows = []
+    for _ in range(KEEP):
+        o.sweep(1)
+        b = o.vector(O.V_BETA)
+        rows.append(np.concatenate([[o.scalar(O.S_SIGMAE), o.scalar(O.S_SIGMAG), np.count_nonzero(b)], b]))
+    return np.array(rows)
+
+
+def _mean_se(a, nb=30):
+    """posterior mean and its Monte-Carlo standard error (batch means)"""
+    a = a[: len(a) // nb * nb].reshape(nb, -1, *a.shape[1:]).mean(axis=1)
+    return a.mean(axis=0), a.std(axis=0, ddof=1) / np.sqrt(nb)
+
+
+def _compare(a, b, big):
+    ma, sa = _mean_se(a)
+    mb, sb = _mean_se(b)
+    z = np.abs(ma - mb) / np.sqrt(sa ** 2 + sb ** 2 + 1e-300)
+    cols = [0, 1, 2] + [3 + j for j in big]  # sigmaE, sigmaG, #non-zero, the large effects
+    return z[cols], ma[cols], mb[cols]
+
+
+@pytest.fixture(scope="module")
+def data(oracle_mod):
+    O = oracle_mod
+    X, Y, beta = O.synth_cohort(20261015, N, P, h2=0.6, n_causal=NC)
+    big = list(np.argsort(-np.abs(beta))[:4])
+    return X, Y, beta, big
+
+
+def test_blocked_scan_matches_reference_order(oracle_mod, data):
+    O = oracle_mod
+    X, Y, beta, big = data
+    ref = _chain(O, X, Y, seed=11, order_mode=O.ORDER_REFERENCE)
+    blk = _chain(O, X, Y, seed=12, order_mode=O.ORDER_BLOCKED, block_size=64)
+    z, ma, mb = _compare(ref, blk, big)
+    assert np.all(z < 4.0), (z, ma, mb)
+    # and the chains see the simulated effects (sign and rough size of the largest ones)
+    assert np.all(np.sign(mb[3:]) == np.sign(beta[big]))
+
+
+def test_column_shards_match_single_shard(oracle_mod, data):
+    O = oracle_mod
+    X, Y, beta, big = data
+    one = _chain(O, X, Y, seed=21, order_mode=O.ORDER_BLOCKED, block_size=64)
+    two = _chain(O, X, Y, seed=22, order_mode=O.ORDER_BLOCKED, block_size=64, n_shards=2)
+    z, ma, mb = _compare(one, two, big)
+    rel = np.abs(ma - mb) / np.abs(ma)
+    assert np.all((z < 4.0) | (rel < 0.03)), (z, rel, ma, mb)
+    assert rel[0] < 0.03 and np.all(z[1:] < 4.0), (z, rel)  # sigmaE within 3 %, the rest within 4 SE
