@@ -1232,13 +1232,17 @@ __device__ __forceinline__ void chain_hs_resident(int bs, const double *Lr0, con
 // is: ballot -> owner lane -> read delta -> update the later positions from the LDS Gram row.
 // A position found outside its window is re-decided at its current num (wave-uniform) and
 // re-examined; an exact-formula position is evaluated by decide_bayesr (BayesRv2.cpp:195-242).
+// coef is the block's Gram in LDS with the entries (i, j) for position i NOT before position j
+// zeroed (chain_coefficients with unit scale), so a step updates every position unconditionally
+// (earlier ones subtract 0) and the fast step has no divergent branch: branches cost the
+// persistent solver far more than their instructions (Horseshoe chain).
 template <int B>
 __device__ __forceinline__ void chain_bayesr_resident(const Dev &d, int bs, double sigmaE, const double *Lr0,
                                                       const double *Llo, const double *Lhi, const double *Ldsel,
                                                       const double *Lsdz, const double *Lbo, double *Lbn,
                                                       const int *Lfl, int *Lks, const int *Lgi, const double *La,
                                                       const double *Lden, const double *Lp, const double *Lx2,
-                                                      const double *Lz, const int *Lm, const double *slots,
+                                                      const double *Lz, const int *Lm, const double *coef,
                                                       bool prof) {
 #pragma clang fp contract(off)
   constexpr int NS = B / 64;
@@ -1260,7 +1264,7 @@ __device__ __forceinline__ void chain_bayesr_resident(const Dev &d, int bs, doub
     sz[q] = in ? Lsdz[pos] : 0.0;
     bo[q] = in ? Lbo[pos] : 0.0;
     bn[q] = bo[q];
-    gg[q] = in ? Lgi[pos] : 0;
+    gg[q] = in ? Lgi[pos] : B - 1;  // past the end: an unused Gram index (zero row and column)
     ks[q] = fl & 0xFF;
     const double tt = r[q] * r[q];
     valid |= (uint32_t)in << q;
@@ -1277,28 +1281,36 @@ __device__ __forceinline__ void chain_bayesr_resident(const Dev &d, int bs, doub
     const uint32_t ge = ALLQ & ~((1u << lowq) - 1u);
     const uint32_t cand = valid & (act | ~win | exb) & ge;
     const int ql = cand ? __builtin_ctz(cand) : 0;
+    // this lane's lowest candidate, by selects (a divergent branch here costs more than all of it)
     double rv = r[0], dvv = dv[0], ivv = iv[0], szv = sz[0], bov = bo[0];
     int ksv = ks[0], ggv = gg[0];
 #pragma unroll
-    for (int q = 1; q < NS; ++q)
-      if (ql == q) { rv = r[q]; dvv = dv[q]; ivv = iv[q]; szv = sz[q]; bov = bo[q]; ksv = ks[q]; ggv = gg[q]; }
-    // speculative new beta of this lane's lowest candidate (BayesRv2.cpp:226-230)
-    const double bnl = ksv == 0 ? 0.0 : (ksv == FALLTHROUGH ? bov : quot_rn(rv, dvv, ivv) + szv);
+    for (int q = 1; q < NS; ++q) {
+      const bool h = ql == q;
+      rv = h ? r[q] : rv;
+      dvv = h ? dv[q] : dvv;
+      ivv = h ? iv[q] : ivv;
+      szv = h ? sz[q] : szv;
+      bov = h ? bo[q] : bov;
+      ksv = h ? ks[q] : ksv;
+      ggv = h ? gg[q] : ggv;
+    }
+    // speculative new beta of this lane's lowest candidate (BayesRv2.cpp:226-230), every arm
+    // evaluated and selected
+    const double qv = quot_rn(rv, dvv, ivv) + szv;
+    const double bnl = ksv == 0 ? 0.0 : (ksv == FALLTHROUGH ? bov : qv);
     const int fastl = (int)(((win & ~exb) >> ql) & 1u);
     const uint64_t bal = __ballot(cand != 0);
     if (!bal) break;  // the rest keep their decisions (no change)
     const int L = __builtin_ctzll(bal);
     const int qf = __builtin_amdgcn_readlane(ql, L);
     const int first = L * NS + qf;  // wave-uniform
-    const double *grow = slots + (int64_t)__builtin_amdgcn_readlane(ggv, L) * B;
+    const double *grow = coef + (int64_t)__builtin_amdgcn_readlane(ggv, L) * B;
     double delta;
-    if (__builtin_amdgcn_readlane(fastl, L)) {
+    if (__builtin_expect(__builtin_amdgcn_readlane(fastl, L) != 0, 1)) {
       delta = readlane_f64(bnl - bov, L);
-      if (lane == L) {
 #pragma unroll
-        for (int q = 0; q < NS; ++q)
-          if (q == qf) bn[q] = bnl;
-      }
+      for (int q = 0; q < NS; ++q) bn[q] = (lane == L && q == qf) ? bnl : bn[q];
     } else {
       const uint64_t ts0 = prof ? wall_clock64() : 0;
       const double rf = readlane_f64(rv, L);
@@ -1336,16 +1348,12 @@ __device__ __forceinline__ void chain_bayesr_resident(const Dev &d, int bs, doub
       ++nslow;
       if (prof) tslow += wall_clock64() - ts0;
     }
-    if (delta != 0.0) {
+    // every position: the row's entries at positions <= first are 0 (and delta may be 0)
 #pragma unroll
-      for (int q = 0; q < NS; ++q) {
-        const int pos = lane * NS + q;
-        if (pos > first && pos < bs) {
-          r[q] = r[q] - grow[gg[q]] * delta;
-          const double tt = r[q] * r[q];
-          win = (win & ~(1u << q)) | ((uint32_t)(tt >= lo[q] && tt <= hi[q]) << q);
-        }
-      }
+    for (int q = 0; q < NS; ++q) {
+      r[q] = r[q] - grow[gg[q]] * delta;
+      const double tt = r[q] * r[q];
+      win = (win & ~(1u << q)) | ((uint32_t)(tt >= lo[q] && tt <= hi[q]) << q);
     }
     i = first + 1;
     ++nsteps;
@@ -1364,10 +1372,15 @@ __device__ __forceinline__ void chain_bayesr_resident(const Dev &d, int bs, doub
   }
 }
 
+#ifndef BRR_EARLY_GRAM
+#define BRR_EARLY_GRAM 0
+#endif
 // persistent: one workgroup solves every block of the sweep in order (LDS persists between blocks)
 template <bool HS, int B, int NT>
+// gi_pref: (persistent) the Gram index of position threadIdx.x % B of the next block, loaded one
+// block ahead so the next block's cross-Gram loads need no dependent round trip
 __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, int nslot, char *smem,
-                                            bool persistent) {
+                                            bool persistent, int &gi_pref) {
 #pragma clang fp contract(off)
   constexpr int NPT = (B + NT - 1) / NT;  // positions per thread, parallel phases
   constexpr int NW = NT / 64;             // waves
@@ -1392,28 +1405,24 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   const int64_t S = d.nbB;
   const int64_t q0 = (int64_t)s * B;
   const bool resident = B <= RESIDENT_BMAX && nslot >= B + solve_scratch_rows(B, NT);
-  // misc[10] / misc[11]: padded length / block of the change list this workgroup left in LDS
-  if (t == 0 && s == 0) misc[11] = -2;
+  // misc[10] / misc[11]: padded length / block of the change list this workgroup left in LDS;
+  // misc[12]: block whose Gram copy into LDS the previous block already started
+  if (t == 0 && s == 0) { misc[11] = -2; misc[12] = -2; }
+  const bool pipelined = persistent && resident;
+  const int gi_t = (pipelined && s >= 1) ? gi_pref : (t % B < bs ? d.gidx[q0 + t % B] : 0);
+  if (pipelined && s + 1 < d.nb) gi_pref = d.gidx[(int64_t)(s + 1) * B + t % B];
 
-  // A) everything that does not depend on k_stream(s).  Resident mode first starts the LDS-DMA of
-  // block s's whole Gram block (the previous block's copy is no longer read: its chain and write-
-  // back are done) so it lands while the constants and the cross-Gram correction are loaded.
-  if (resident) {
-    // row gi at slots + gi B, 1 KiB per wave-instruction; retired by each wave's vmcnt(0) and the
-    // barrier after it (before the coefficients / decisions read it)
-    constexpr int NCHUNK = B * B * 8 / 1024;
-    const char *src = reinterpret_cast<const char *>(d.gram + (int64_t)gb * B * B);
-    char *dst = reinterpret_cast<char *>(slots);
-    for (int c = wv; c < NCHUNK; c += NW)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + c * 1024 + lane * 16),
-                                       (__attribute__((address_space(3))) void *)(dst + c * 1024), 16, 0, 0);
-  }
+  // A) everything that does not depend on k_stream(s).  The per-position constants are loaded
+  // first (vmcnt retires loads in order, so loads issued behind the 128 KiB Gram copy would wait
+  // for all of it), then resident mode starts the LDS-DMA of block s's Gram block (the previous
+  // block's copy is no longer read: its chain and write-back are done) so it lands while the
+  // cross-Gram correction is formed.
 #pragma unroll
   for (int c = 0; c < NPT; ++c) {
     const int pos = t + NT * c;
     if (pos < bs) {
       const int64_t q = q0 + pos;
-      const int gi = d.gidx[q];
+      const int gi = NPT == 1 ? gi_t : d.gidx[q];
       double av[MAXK], dv[MAXK];
 #pragma unroll
       for (int k = 0; k < MAXK; ++k) {
@@ -1435,6 +1444,18 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       }
     }
   }
+  if (resident && !(pipelined && s >= 1 && misc[12] == s)) {
+    // row gi at slots + gi B, 1 KiB per wave-instruction; retired by each wave's vmcnt(0) and the
+    // barrier after it (before the coefficients / decisions read it).  (The persistent solver
+    // starts this copy at the end of the previous block already, see step 3.)
+    constexpr int NCHUNK = B * B * 8 / 1024;
+    const char *src = reinterpret_cast<const char *>(d.gram + (int64_t)gb * B * B);
+    char *dst = reinterpret_cast<char *>(slots);
+    for (int c = wv; c < NCHUNK; c += NW)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + c * 1024 + lane * 16),
+                                       (__attribute__((address_space(3))) void *)(dst + c * 1024), 16, 0, 0);
+  }
+  const uint64_t tA1 = prof ? wall_clock64() : 0;  // constants loaded (this thread's)
   // sum_i (x_j . x_i) delta_i over the changes of the blocks the streamed dots have not seen:
   // block s-1 (cross-Gram of cycle neighbours), and with lag 2 also block s-2 (cross-Gram of
   // blocks two apart), added in that order.  Each change list (padded to a multiple of 16) is
@@ -1484,7 +1505,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       const int c0 = grp * nch / PG, c1 = (grp + 1) * nch / PG;
       double corr = 0.0;
       if (pos < bs) {
-        const int gi = Lgi[pos];
+        const int gi = NPT == 1 ? gi_t : Lgi[pos];
         // two chunks (32 loads) in flight, added in list order
         for (int ch = c0; ch < c1; ch += 2) {
           const bool two = ch + 1 < c1;
@@ -1519,23 +1540,23 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       }
     }
   }
-  if constexpr (HS) {
-    if (resident) {
-      // the chain's coefficients (G_ij / D_j for i before j, else 0) made in place from the
-      // resident Gram before the wait for the streaming side (D is a per-sweep constant of the
-      // Horseshoe, HorseshoeR.cpp:226-232); the scratch behind the rows holds RN(1/D) and the
-      // position of every Gram index
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces landed
-      __syncthreads();  // (also: the correction's partial sums in the scratch are consumed)
-      double *Linv = scr;
-      int *Lposg = reinterpret_cast<int *>(scr + B);
-      for (int g = t; g < B; g += NT) { Linv[g] = 0.0; Lposg[g] = B; }
-      __syncthreads();
-      for (int pos = t; pos < bs; pos += NT) { Linv[Lgi[pos]] = 1.0 / La[pos]; Lposg[Lgi[pos]] = pos; }
-      __syncthreads();
-      chain_coefficients<B, NT>(slots, Linv, Lposg);
-    }
+  const uint64_t tA2 = prof ? wall_clock64() : 0;  // cross-Gram correction done
+  if (resident) {
+    // the chain's coefficients made in place from the resident Gram before the wait for the
+    // streaming side: entry (i, j) = G_ij / D_j (Horseshoe: D is a per-sweep constant,
+    // HorseshoeR.cpp:226-232) or G_ij (BayesR) when position i comes before position j, else 0;
+    // the scratch behind the rows holds the scale and the position of every Gram index
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces landed
+    __syncthreads();  // (also: the correction's partial sums in the scratch are consumed)
+    double *Linv = scr;
+    int *Lposg = reinterpret_cast<int *>(scr + B);
+    for (int g = t; g < B; g += NT) { Linv[g] = 0.0; Lposg[g] = B; }
+    __syncthreads();
+    for (int pos = t; pos < bs; pos += NT) { Linv[Lgi[pos]] = HS ? 1.0 / La[pos] : 1.0; Lposg[Lgi[pos]] = pos; }
+    __syncthreads();
+    chain_coefficients<B, NT>(slots, Linv, Lposg);
   }
+  const uint64_t tA3 = prof ? wall_clock64() : 0;  // coefficients built
   // B) wait for k_stream(s)'s reduction groups (other queue; cumulative count)
   if (t == 0 && s == 0) stamp(d.sync, 3);
   if (t == 0) wait_geq(d.sync + SY_GDONE + 32 * par, (d.gbase[par] + s / NPAR + 1) * d.gtarget, d.sync, 3);
@@ -1861,6 +1882,21 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   __syncthreads();
   if (prof) tp3 = wall_clock64();
   const uint64_t tc3 = prof ? __builtin_amdgcn_s_memtime() : 0;
+  if (BRR_EARLY_GRAM && pipelined && s + 1 < d.nb) {
+    // this block's coefficients are no longer read: the upper half of the waves starts copying
+    // the next block's Gram block into LDS, in flight during the write-back and the next block's
+    // constants and cross-Gram loads.  (Measured slower: every barrier of the write-back then waits
+    // for the copy -- a workgroup barrier retires outstanding LDS-DMA -- so it is off by default.)
+    if (wv >= NW / 2) {
+      constexpr int NCHUNK = B * B * 8 / 1024;
+      const char *src = reinterpret_cast<const char *>(d.gram + (int64_t)d.gblk[s + 1] * B * B);
+      char *dst = reinterpret_cast<char *>(slots);
+      for (int c = wv - NW / 2; c < NCHUNK; c += NW / 2)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + c * 1024 + lane * 16),
+                                         (__attribute__((address_space(3))) void *)(dst + c * 1024), 16, 0, 0);
+    }
+    if (t == 0) misc[12] = s + 1;
+  }
   // 4) write back, compact the changed markers into this block's list (position order)
   const int pslot = s % NSLOT;
   int *pidx = d.pend_idx + pslot * d.pend_stride, *pgi = d.pend_gi + pslot * d.pend_stride;
@@ -1922,8 +1958,10 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     st_sc1_int(d.pend_n + pslot, npad);
     st_sc1_int(d.pend_n + NSLOT + pslot, npend);
   }
-  // publish: every storing wave drains its sc1 stores, then the block count (k_stream(s+2))
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // publish: every storing wave drains its sc1 stores, then the block count (k_stream(s+2)).  The
+  // stores above come from the position threads (t < B) only; with B <= NT / 2 the upper half of
+  // the waves stored nothing and must not wait here for the next block's Gram copy it started
+  if (!(pipelined && B <= NT / 2 && wv >= NW / 2)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0) {
     __hip_atomic_store(d.sync + SY_PEND, d.sbase + s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1939,6 +1977,9 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       atomicAdd(&d.sc->prof[3], (unsigned long long)(tp4 - tp3));
       atomicAdd(&d.sc->prof[5], 1ull);
       atomicAdd(&d.sc->prof[10], (unsigned long long)(tw - tp0));
+      atomicAdd(&d.sc->prof[13], (unsigned long long)(tA1 - tp0));
+      atomicAdd(&d.sc->prof[14], (unsigned long long)(tA2 - tA1));
+      atomicAdd(&d.sc->prof[15], (unsigned long long)(tA3 - tA2));
       atomicAdd(&d.sc->prof[11], (unsigned long long)(tc3 - tc2));
     }
   }
@@ -1947,7 +1988,8 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
 template <bool HS, int B>
 __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it, int nslot) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  solve_block<HS, B, 256>(d, s, it, nslot, smem, false);
+  int gi_pref = 0;
+  solve_block<HS, B, 256>(d, s, it, nslot, smem, false, gi_pref);
 }
 
 
@@ -2356,8 +2398,9 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
 
 template <bool HS, int B>
 __device__ __forceinline__ void solver_role(const Dev &d, uint32_t it, int nslot, char *smem) {
+  int gi_pref = 0;
   for (int s = 0; s < d.nb; ++s) {
-    solve_block<HS, B, SWEEP_NT>(d, s, it, nslot, smem, true);
+    solve_block<HS, B, SWEEP_NT>(d, s, it, nslot, smem, true, gi_pref);
     __syncthreads();
   }
 }

@@ -406,6 +406,9 @@ def main():
         diag["solve_refresh_us"] = round(s.scalar(118) / calls / 100.0, 3)
         diag["solve_correct_us"] = round(s.scalar(119) / calls / 100.0, 3)
         diag["solve_wait_us"] = round(s.scalar(120) / calls / 100.0, 3)
+        # phase A (thread 0's view): constants, cross-Gram correction, resident coefficients
+        diag["solve_phaseA_us"] = {k: round(s.scalar(123 + i) / calls / 100.0, 3) for i, k in
+                                   enumerate(["constants", "correction", "coefficients"])}
         # shader clock during the chain: s_memtime ticks / s_memrealtime (100 MHz) ticks
         diag["solve_chain_clock_ghz"] = round(s.scalar(121) / max(1.0, s.scalar(112)) * 0.1, 3)
         # serial chain loop alone (shader clocks per chain step; wave 0 of the solver)
