@@ -10,10 +10,10 @@ from ._lib import (ABI_VERSION, BrrError, MODEL_GROUPS, MODEL_HORSESHOE, MODEL_R
                    MODEL_V2, ORDER_BLOCKED, ORDER_IDENTITY, ORDER_REFERENCE, lib)
 from .build import LIB_PATH, build_library
 from .samplers import BRV2Grstart, BayesRSamplerV2, BayesRSamplerV2Groups, HorseshoeR
-from .session import Session
+from .session import Group, Session
 
 __all__ = [
     "ABI_VERSION", "BrrError", "MODEL_V2", "MODEL_GROUPS", "MODEL_RESTART", "MODEL_HORSESHOE",
     "ORDER_BLOCKED", "ORDER_REFERENCE", "ORDER_IDENTITY", "lib", "LIB_PATH", "build_library",
-    "BayesRSamplerV2", "BayesRSamplerV2Groups", "BRV2Grstart", "HorseshoeR", "Session",
+    "BayesRSamplerV2", "BayesRSamplerV2Groups", "BRV2Grstart", "HorseshoeR", "Session", "Group",
 ]

@@ -16,7 +16,7 @@ ORDER_BLOCKED, ORDER_REFERENCE, ORDER_IDENTITY = 0, 1, 2
 X_F32, X_2BIT = 0, 1  # brr_x_storage
 (MU, SIGMAE, SIGMAG, SIGMAF, TAU, ETA, C2, SUMSQ_BETA) = range(8)
 (BETA, COMP, EPS, SIGMAGG, PI, ALPHA, LAMBDA, XSQ, ORDER, VCOUNT, BETAACUM, HSV) = range(12)
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 LOG_FN = C.CFUNCTYPE(None, C.c_char_p, C.c_void_p)
 
@@ -31,6 +31,8 @@ class Options(C.Structure):
         ("order_mode", C.c_int32), ("shard_rank", C.c_int32), ("shard_count", C.c_int32),
         ("verbose", C.c_int32), ("x_storage", C.c_int32),
         ("log", LOG_FN), ("log_userdata", C.c_void_p),
+        ("row_shard_rank", C.c_int32), ("row_shard_count", C.c_int32),
+        ("row_offset", C.c_int64), ("N_total", C.c_int64),
     ]
 
 
@@ -50,6 +52,7 @@ EXPORTED = [
     "brr_session_set_vector", "brr_session_set_scalar", "brr_session_iteration",
     "brr_session_set_timing", "brr_session_timing", "brr_session_block_size",
     "brr_session_synchronize", "brr_session_linear_predictor",
+    "brr_group_create", "brr_group_init", "brr_group_sweep", "brr_group_destroy",
 ]
 
 _lib = None
@@ -125,6 +128,11 @@ def lib():
     L.brr_session_block_size.argtypes = [vp]
     L.brr_session_synchronize.argtypes = [vp]
     L.brr_session_linear_predictor.argtypes = [vp, D]
+    L.brr_group_create.restype = vp
+    L.brr_group_create.argtypes = [C.POINTER(vp), C.c_int32]
+    L.brr_group_init.argtypes = [vp, C.c_int32]
+    L.brr_group_sweep.argtypes = [vp, C.c_int32]
+    L.brr_group_destroy.argtypes = [vp]
     _lib = L
     return L
 
@@ -141,12 +149,15 @@ def check(rc: int, what: str) -> int:
 
 
 def options(device=0, block_size=0, order_mode=ORDER_BLOCKED, shard_rank=0, shard_count=1,
-            verbose=0, log=None, x_storage=X_F32) -> Options:
+            verbose=0, log=None, x_storage=X_F32, row_shard_rank=0, row_shard_count=1, row_offset=0,
+            N_total=0) -> Options:
     o = Options()
     lib().brr_options_default(C.byref(o))
     o.device, o.block_size, o.order_mode = device, block_size, order_mode
     o.shard_rank, o.shard_count, o.verbose = shard_rank, shard_count, verbose
     o.x_storage = x_storage
+    o.row_shard_rank, o.row_shard_count = row_shard_rank, row_shard_count
+    o.row_offset, o.N_total = row_offset, N_total
     if log is not None:
         cb = LOG_FN(lambda msg, _u: log(msg.decode()))
         o.log = cb

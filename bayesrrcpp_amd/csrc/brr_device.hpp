@@ -34,11 +34,19 @@ constexpr int FALLTHROUGH = 255;  // no component selected (700-guard, BayesRv2.
 
 enum Model : int { MODEL_V2 = 0, MODEL_GROUPS = 1, MODEL_RESTART = 2, MODEL_HORSESHOE = 3 };
 
+// In-process row-shard group (brr_group): the members' copies of one buffer, rank order.
+constexpr int GROUP_MAX = 16;
+struct GroupPtrs {
+  double *ptr[GROUP_MAX];
+  int n;
+};
+
 // Device-resident scalar state of a chain.
 struct Scal {
   double mu, mu_prev, sigmaE, sigmaF, tau, eta, c2;
   double S1;   // sum(eps + mu)   (BayesRv2.cpp:177-178 operand), from the latest row pass
   double S2;   // ||eps||^2        (BayesRv2.cpp:251 operand)
+  double fx;   // row shards: this shard's part of a fixed-effect dot (BayesRv2Groups.cpp:220), summed across shards
   int pad0, pad1;
   unsigned long long n_slow;     // diagnostics: serial steps that needed the exact re-evaluation
   unsigned long long n_changed;  // diagnostics: markers whose beta changed
@@ -81,6 +89,7 @@ __host__ __device__ inline int stats_size(int G, int K) { return 2 + G + G * K; 
 // Everything a kernel needs: dimensions, hyper-parameters and device pointers (by value).
 struct Dev {
   int64_t N, ld, M, M_total, col_offset;
+  int64_t Ntot, row_offset;  // row shards: cohort rows and this shard's first row (else N, 0)
   int K, G, F, B, nb, model, R, RG, NG, MRG;
   int gtarget;      // reduction groups k_solve(s) waits for (per-block: NG * NC; persistent: NG)
   uint64_t seed;

@@ -219,8 +219,10 @@ __device__ __forceinline__ int genotype(uint64_t ds, int64_t i, int64_t j, uint3
 }
 
 // f32 storage (X) or 2-bit codes (Xc, code = genotype, 3 = padding) + value table (xlut).
+// Row shards: the column statistics run over all Ntot rows of the cohort (the
+// genotypes are counter-based, so every shard draws them), only rows [row0, row0 + N) are stored.
 __global__ __launch_bounds__(256) void k_synth_x(float *X, uint8_t *Xc, float *xlut, int64_t ld, int64_t ldc,
-                                                 int64_t N, int64_t col0, uint64_t ds) {
+                                                 int64_t N, int64_t col0, uint64_t ds, int64_t Ntot, int64_t row0) {
 #pragma clang fp contract(off)
   __shared__ double red[8];
   __shared__ int s_att;
@@ -234,20 +236,20 @@ __global__ __launch_bounds__(256) void k_synth_x(float *X, uint8_t *Xc, float *x
   double S = 0.0, Q = 0.0;
   for (; att < 16; ++att) {
     double s = 0.0, q = 0.0;
-    for (int64_t i = threadIdx.x; i < N; i += 256) {
+    for (int64_t i = threadIdx.x; i < Ntot; i += 256) {
       int g = genotype(ds, i, j, att, t0, t1);
       s += g;
       q += g * g;
     }
     S = block_sum<256>(s, red);
     Q = block_sum<256>(q, red);
-    if (N > 1 && Q * (double)N != S * S) break;
+    if (Ntot > 1 && Q * (double)Ntot != S * S) break;
   }
   if (threadIdx.x == 0) s_att = (int)att;
   __syncthreads();
-  const bool mono = s_att == 16 || N < 2;
-  const double mean = S / (double)N;
-  const double var = (Q - S * S / (double)N) / (double)(N - 1);
+  const bool mono = s_att == 16 || Ntot < 2;
+  const double mean = S / (double)Ntot;
+  const double var = (Q - S * S / (double)Ntot) / (double)(Ntot - 1);
   const double sd = sqrt(var);
   if (Xc) {
     // value of genotype g = f32((g - mean) / sd), exactly the f32 storage's value
@@ -261,7 +263,7 @@ __global__ __launch_bounds__(256) void k_synth_x(float *X, uint8_t *Xc, float *x
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int64_t i = 4 * b + k;
-        const uint32_t c = (mono || i >= N) ? 3u : (uint32_t)genotype(ds, i, j, att, t0, t1);
+        const uint32_t c = (mono || i >= N) ? 3u : (uint32_t)genotype(ds, row0 + i, j, att, t0, t1);
         byte |= c << (2 * k);
       }
       xc[b] = (uint8_t)byte;
@@ -274,7 +276,7 @@ __global__ __launch_bounds__(256) void k_synth_x(float *X, uint8_t *Xc, float *x
   }
   for (int64_t i = threadIdx.x; i < ld; i += 256) {
     float v = 0.f;
-    if (i < N) v = (float)(((double)genotype(ds, i, j, att, t0, t1) - mean) / sd);
+    if (i < N) v = (float)(((double)genotype(ds, row0 + i, j, att, t0, t1) - mean) / sd);
     x[i] = v;
   }
 }
@@ -456,7 +458,7 @@ __global__ void k_sweep_start(Dev d, uint32_t it) {
   Scal *sc = d.sc;
   sc->mu_prev = sc->mu;
   const double z = normal(d.seed, T_MU, 0, it, 0);
-  sc->mu = sc->S1 / (double)d.N + sqrt(sc->sigmaE / (double)d.N) * z;
+  sc->mu = sc->S1 / (double)d.Ntot + sqrt(sc->sigmaE / (double)d.Ntot) * z;  // all rows (row shards: summed S1)
   if (d.model == MODEL_HORSESHOE) {
     const Hyper &h = d.hyp;
     sc->eta = inv_gamma_rate_rng(d.seed, 0.5 + 0.5 * h.vT,
@@ -537,7 +539,7 @@ __global__ __launch_bounds__(1024) void k_fixed(Dev d, uint32_t it, int perm_on_
     }
     const double num_f = block_sum<1024>(part, red);
     const double sigmaE = d.sc->sigmaE;
-    const double denom_f = (double)(N - 1) + (sigmaE / d.sc->sigmaF);
+    const double denom_f = (double)(d.Ntot - 1) + (sigmaE / d.sc->sigmaF);
     const double z = normal(d.seed, T_FIXED, (uint32_t)cur, it, 0);
     const double an = num_f / denom_f + sqrt(sigmaE / denom_f) * z;
     for (int64_t i = threadIdx.x; i < N; i += 1024) {
@@ -547,6 +549,78 @@ __global__ __launch_bounds__(1024) void k_fixed(Dev d, uint32_t it, int perm_on_
     __syncthreads();
     if (threadIdx.x == 0) d.alpha[cur] = an;
     __syncthreads();
+  }
+}
+
+// Row shards: fixed effect cf of the sweep in two launches around the cross-shard
+// sum of the dot product f . (eps + f alpha) (BayesRv2Groups.cpp:218-224).  Phase 0 forms this
+// shard's part (into sc->fx; cf == 0 also draws the sweep's fixed-effect order), phase 1 draws
+// alpha from the summed dot (identical on every shard) and updates this shard's residual rows.
+// With one shard it performs k_fixed's operations in k_fixed's order.
+__global__ __launch_bounds__(1024) void k_fixed_row(Dev d, uint32_t it, int cf, int phase, int perm_on_device) {
+#pragma clang fp contract(off)
+  __shared__ double red[16];
+  __shared__ int ford[1024];
+  const int F = d.F;
+  if (F > 1024) return;
+  if (phase == 0 && cf == 0) {
+    if (threadIdx.x == 0) {
+      for (int f = 0; f < F; ++f) ford[f] = perm_on_device ? f : d.forder[f];
+      if (perm_on_device) fisher_yates_dev(d.seed, ford, F, T_PERM_FIXED, 0, it);
+    }
+    __syncthreads();
+    for (int f = threadIdx.x; f < F; f += 1024) d.forder[f] = ford[f];  // read by the later launches
+  } else if (threadIdx.x == 0) {
+    ford[cf] = d.forder[cf];
+  }
+  __syncthreads();
+  const int64_t N = d.N;
+  const int cur = ford[cf];
+  const double *f = d.fixed + (int64_t)cur * N;
+  const double ca = d.alpha[cur];
+  if (phase == 0) {
+    double part = 0.0;
+    for (int64_t i = threadIdx.x; i < N; i += 1024) {
+      const double yt = d.eps[i] + f[i] * ca;
+      part += f[i] * yt;
+    }
+    const double num_f = block_sum<1024>(part, red);
+    if (threadIdx.x == 0) d.sc->fx = num_f;
+    return;
+  }
+  const double num_f = d.sc->fx;
+  const double sigmaE = d.sc->sigmaE;
+  const double denom_f = (double)(d.Ntot - 1) + (sigmaE / d.sc->sigmaF);
+  const double z = normal(d.seed, T_FIXED, (uint32_t)cur, it, 0);
+  const double an = num_f / denom_f + sqrt(sigmaE / denom_f) * z;
+  for (int64_t i = threadIdx.x; i < N; i += 1024) {
+    const double yt = d.eps[i] + f[i] * ca;
+    d.eps[i] = yt - f[i] * an;
+  }
+  if (threadIdx.x == 0) d.alpha[cur] = an;
+}
+
+// Row shards: block s's level-2 partial dots (slab2 rows 0 .. NG-1 of ring index s % NPAR)
+// summed into row 0, in group order -- the order in which k_solve sums them -- so the value the
+// solver reads with NG = 1 after the cross-shard sum is, on one shard, bit-identical to its own.
+__global__ void k_slab_total(Dev d, int s) {
+#pragma clang fp contract(off)
+  double *slab2 = d.slab2 + (s % NPAR) * d.slab2_stride;
+  for (int pos = threadIdx.x; pos < d.B; pos += blockDim.x) {
+    double acc = 0.0;
+    for (int g = 0; g < d.NG; ++g) acc += slab2[(int64_t)g * d.B + pos];
+    slab2[pos] = acc;
+  }
+}
+
+// In-process row-shard group: sum of the members' buffers in rank order, written back to every
+// member (one device, or peer-mapped devices).
+__global__ __launch_bounds__(256) void k_group_sum(GroupPtrs p, int64_t n) {
+#pragma clang fp contract(off)
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    double acc = p.ptr[0][i];
+    for (int r = 1; r < p.n; ++r) acc += p.ptr[r][i];
+    for (int r = 0; r < p.n; ++r) p.ptr[r][i] = acc;
   }
 }
 
@@ -2533,7 +2607,7 @@ __global__ void k_hyper(Dev d, uint32_t it, const double *stats) {
   Scal *sc = d.sc;
   const Hyper &h = d.hyp;
   const int G = d.G, K = d.K;
-  const double N = (double)d.N;
+  const double N = (double)d.Ntot;
   const double *bacc = stats + 2;
   const double *v = stats + 2 + G;
   const double sigmaE_new = inv_scaled_chisq_rng(d.seed, h.v0E + N, (sc->S2 + h.v0E * h.s02E) / (h.v0E + N),
@@ -2587,7 +2661,7 @@ __global__ void k_hyper_init(Dev d, const double *stats, int pi_given) {
   Scal *sc = d.sc;
   const Hyper &h = d.hyp;
   const int G = d.G, K = d.K;
-  const double N = (double)d.N;
+  const double N = (double)d.Ntot;
   if (d.model != MODEL_RESTART && t == 0) sc->sigmaE = sc->S2 / N * 0.5;
   if (d.model == MODEL_V2 && t == 0) d.sigmaGG[0] = uniform(d.seed, T_INIT, 0, INIT_IT, 0);
   if (d.model == MODEL_GROUPS) {
@@ -2638,7 +2712,8 @@ static inline unsigned cdiv64(int64_t a, int64_t b) { return (unsigned)((a + b -
 
 hipError_t launch_synth_x(const Dev &d, uint64_t ds, hipStream_t st) {
   hipLaunchKernelGGL(k_synth_x, dim3((unsigned)d.M), dim3(256), 0, st, const_cast<float *>(d.X),
-                     const_cast<uint8_t *>(d.Xc), const_cast<float *>(d.xlut), d.ld, d.ldc, d.N, d.col_offset, ds);
+                     const_cast<uint8_t *>(d.Xc), const_cast<float *>(d.xlut), d.ld, d.ldc, d.N, d.col_offset, ds,
+                     d.Ntot, d.row_offset);
   return hipGetLastError();
 }
 
@@ -2704,6 +2779,23 @@ hipError_t launch_lut_order(const Dev &d, hipStream_t st) {
 
 hipError_t launch_fixed(const Dev &d, uint32_t it, bool perm_on_device, hipStream_t st) {
   hipLaunchKernelGGL(k_fixed, dim3(1), dim3(1024), 0, st, d, it, perm_on_device ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_fixed_row(const Dev &d, uint32_t it, int cf, int phase, bool perm_on_device, hipStream_t st) {
+  hipLaunchKernelGGL(k_fixed_row, dim3(1), dim3(1024), 0, st, d, it, cf, phase, perm_on_device ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_slab_total(const Dev &d, int s, hipStream_t st) {
+  hipLaunchKernelGGL(k_slab_total, dim3(1), dim3(BMAX), 0, st, d, s);
+  return hipGetLastError();
+}
+
+hipError_t launch_group_sum(const GroupPtrs &p, int64_t n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const unsigned grid = cdiv64(n, 256) > 1024 ? 1024 : cdiv64(n, 256);
+  hipLaunchKernelGGL(k_group_sum, dim3(grid), dim3(256), 0, st, p, n);
   return hipGetLastError();
 }
 

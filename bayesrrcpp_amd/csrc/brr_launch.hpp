@@ -26,6 +26,10 @@ hipError_t launch_noop(hipStream_t st);
 hipError_t launch_perm(const Dev &d, uint32_t it, int shard, bool identity, hipStream_t st);
 hipError_t launch_fixed(const Dev &d, uint32_t it, bool perm_on_device, hipStream_t st);
 hipError_t launch_stream(const Dev &d, int s, const double *eps_in, double *eps_out, hipStream_t st);
+// row shards
+hipError_t launch_fixed_row(const Dev &d, uint32_t it, int cf, int phase, bool perm_on_device, hipStream_t st);
+hipError_t launch_slab_total(const Dev &d, int s, hipStream_t st);
+hipError_t launch_group_sum(const GroupPtrs &p, int64_t n, hipStream_t st);
 hipError_t launch_prep(const Dev &d, uint32_t it, hipStream_t st);
 struct FusedCfg {
   int nsg = 0, rpw = 0, npass = 0, nslot = 0, ngroups = 0, nred = 0;

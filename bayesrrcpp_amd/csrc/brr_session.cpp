@@ -12,6 +12,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -127,6 +128,8 @@ struct brr_session {
   int K = 1, G = 1, F = 0, B = 128, nb = 0, model = 0, NS = 0;
   int order_mode = BRR_ORDER_BLOCKED;
   int shard = 0, nshard = 1;
+  int rshard = 0, nrshard = 1;  // exact row shards: this session's rank / count
+  hipEvent_t ev_x = nullptr;    // row shards in one process (brr_group): cross-stream ordering
   int32_t iteration = 0;
   bool initialized = false, pi_given = false, need_reduce = false, have_y = false, have_x = false;
   bool x2bit = false;  // genotype storage: 2-bit codes (opt.x_storage == BRR_X_2BIT)
@@ -158,6 +161,7 @@ struct brr_session {
     if (comm) (void)ncclCommDestroy(comm);
     for (void *p : allocs) (void)hipFree(p);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
+    if (ev_x) (void)hipEventDestroy(ev_x);
     if (st) (void)hipStreamDestroy(st);
   }
   hipEvent_t ev() {
@@ -385,6 +389,267 @@ int d2h(brr_session *s, T *dst, const T *src, int64_t n) {
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// Exact row shards.  A Coll is the set of sessions one host thread drives: one
+// session (single GPU; or one row shard of a multi-process RCCL job) or every member of an
+// in-process brr_group.  coll_sum is the exchange step: the sum across row shards of a device
+// buffer, in place, identical on every shard -- ncclAllReduce on the session stream (one process
+// per GPU), or k_group_sum over the members' buffers in rank order (brr_group), ordered against
+// the members' streams with events.  Without row shards it does nothing.
+struct Coll {
+  std::vector<brr_session *> ss;
+  bool rows() const { return ss[0]->nrshard > 1; }
+};
+
+template <class Get>
+int coll_sum(Coll &c, Get get, int64_t n) {
+  if (!c.rows() || n <= 0) return 0;
+  if (c.ss.size() == 1) {
+    brr_session *s = c.ss[0];
+    if (!s->comm) {
+      set_error("row-sharded session without a communicator: brr_session_comm_init before init, or a brr_group");
+      return -1;
+    }
+    double *b = get(s);
+    const ncclResult_t r = ncclAllReduce(b, b, (size_t)n, ncclDouble, ncclSum, s->comm, s->st);
+    if (r != ncclSuccess) { set_error("ncclAllReduce (row shards): %s", ncclGetErrorString(r)); return -2; }
+    return 0;
+  }
+  brr_session *s0 = c.ss[0];
+  GroupPtrs p{};
+  p.n = (int)c.ss.size();
+  for (size_t i = 0; i < c.ss.size(); ++i) {
+    p.ptr[i] = get(c.ss[i]);
+    if (i > 0) {
+      HIPCHK(hipSetDevice(c.ss[i]->device));
+      HIPCHK(hipEventRecord(c.ss[i]->ev_x, c.ss[i]->st));
+      HIPCHK(hipSetDevice(s0->device));
+      HIPCHK(hipStreamWaitEvent(s0->st, c.ss[i]->ev_x, 0));
+    }
+  }
+  HIPCHK(hipSetDevice(s0->device));
+  HIPCHK(launch_group_sum(p, n, s0->st));
+  HIPCHK(hipEventRecord(s0->ev_x, s0->st));
+  for (size_t i = 1; i < c.ss.size(); ++i) {
+    HIPCHK(hipSetDevice(c.ss[i]->device));
+    HIPCHK(hipStreamWaitEvent(c.ss[i]->st, s0->ev_x, 0));
+  }
+  return 0;
+}
+
+// f(s) for every session of the collective, on its device
+template <class F>
+int coll_each(Coll &c, F f) {
+  for (brr_session *s : c.ss) {
+    HIPCHK(hipSetDevice(s->device));
+    if (int rc = f(s)) return rc;
+  }
+  return 0;
+}
+
+double *sc_sums(brr_session *s) { return &s->d.sc->S1; }  // S1, S2: adjacent in Scal
+
+// the Gram and cross-Gram blocks of the current layout (init; REFERENCE order: every sweep),
+// summed over the row shards
+int coll_grams(Coll &c) {
+  if (int rc = coll_each(c, [](brr_session *s) -> int {
+        Dev &d = s->d;
+        HIPCHK(launch_gram(d, 0, d.gram, nullptr, s->st));
+        HIPCHK(launch_gram(d, 1, d.xgram, d.xgramT, s->st));  // cycle neighbours (b, b+1 mod nb)
+        if (d.lag >= 2) HIPCHK(launch_gram(d, 2, d.xgram2, d.xgram2T, s->st));  // (b, b+2 mod nb)
+        if (d.lag >= 3) HIPCHK(launch_gram(d, 3, d.xgram3, d.xgram3T, s->st));  // (b, b+3 mod nb)
+        return 0;
+      }))
+    return rc;
+  if (!c.rows()) return 0;
+  const int64_t nbb = (int64_t)c.ss[0]->nb * c.ss[0]->B * c.ss[0]->B;
+  if (int rc = coll_sum(c, [](brr_session *s) { return s->d.gram; }, nbb)) return rc;
+  if (int rc = coll_sum(c, [](brr_session *s) { return s->d.xgram; }, nbb)) return rc;
+  return coll_sum(c, [](brr_session *s) { return s->d.xgramT; }, nbb);
+}
+
+int coll_init(Coll &c, int32_t seed) {
+  for (brr_session *s : c.ss) {
+    if (!s->have_x) { set_error("X not uploaded"); return -1; }
+    if (s->model != MODEL_RESTART && !s->have_y) { set_error("Y not set"); return -1; }
+  }
+  // identity block layout -> Gram blocks and xsquared (BayesRv2.cpp:170)
+  if (int rc = coll_each(c, [&](brr_session *s) -> int {
+        s->d.seed = (uint64_t)(int64_t)seed;
+        HIPCHK(launch_perm(s->d, 0, s->shard, true, s->st));
+        return 0;
+      }))
+    return rc;
+  if (int rc = coll_grams(c)) return rc;
+  if (int rc = coll_each(c, [](brr_session *s) -> int {
+        Dev &d = s->d;
+        HIPCHK(launch_xsq(d, s->st));
+        Scal sc{};
+        if (s->model == MODEL_RESTART) { sc.mu = s->mu0; sc.sigmaE = s->sigmaE0; }
+        if (s->model == MODEL_HORSESHOE) sc.c2 = d.hyp.c2_0;
+        HIPCHK(hipMemcpyAsync(d.sc, &sc, sizeof sc, hipMemcpyHostToDevice, s->st));
+        if (s->model != MODEL_RESTART) {
+          HIPCHK(hipMemsetAsync(d.beta, 0, sizeof(double) * s->M, s->st));
+          HIPCHK(hipMemsetAsync(d.comp, 0, sizeof(int) * s->M, s->st));
+        }
+        HIPCHK(hipMemsetAsync(d.sel, 0, s->M, s->st));
+        HIPCHK(hipMemsetAsync(d.alpha, 0, sizeof(double) * std::max(s->F, 1), s->st));
+        if (s->F > 0)  // identity fixed-effect order (IDENTITY mode; REFERENCE overwrites per sweep)
+          if (int rc = h2d(s, d.forder, s->ref_forder.data(), s->F)) return rc;
+        if (s->model == MODEL_HORSESHOE) {
+          std::vector<double> ones((size_t)s->M, 1.0);
+          if (int rc = h2d(s, d.lambda, ones.data(), s->M)) return rc;
+          if (int rc = h2d(s, d.hsv, ones.data(), s->M)) return rc;
+        }
+        return rows_flagged(s, (s->model == MODEL_RESTART ? 0 : (H_ROW_INIT_Y | H_ROW_WRITE)) | H_ROW_REDUCE);
+      }))
+    return rc;
+  if (int rc = coll_sum(c, sc_sums, 2)) return rc;
+  return coll_each(c, [](brr_session *s) -> int {
+    Dev &d = s->d;
+    if (s->model == MODEL_RESTART) {
+      if (s->nshard > 1) { set_error("restart across column shards needs summed counts: not supported"); return -1; }
+      HIPCHK(launch_markers(d, H_MR_COUNT_ALL, 0, s->st));  // every row shard holds every marker
+    }
+    HIPCHK(launch_hyper_init(d, d.stats, s->pi_given, s->st));
+    HIPCHK(hipStreamSynchronize(s->st));
+    s->iteration = 0;
+    s->initialized = true;
+    s->need_reduce = false;
+    return 0;
+  });
+}
+
+// One exact sweep of row-sharded sessions (per-block kernels; the same operations as
+// do_sweep_local + do_sweep_finish with the cross-shard sums inserted where a quantity runs over
+// rows: residual sums, fixed-effect dots, each block's dots, and REFERENCE order's Gram blocks).
+int coll_sweep_rows(Coll &c) {
+  for (brr_session *s : c.ss)
+    if (!s->initialized) { set_error("session not initialised"); return -1; }
+  bool red = false;
+  for (brr_session *s : c.ss) red |= s->need_reduce;
+  if (red) {
+    if (int rc = coll_each(c, [](brr_session *s) -> int {
+          s->need_reduce = false;
+          return rows_flagged(s, H_ROW_REDUCE);
+        }))
+      return rc;
+    if (int rc = coll_sum(c, sc_sums, 2)) return rc;
+  }
+  brr_session *s0 = c.ss[0];
+  const uint32_t it = (uint32_t)s0->iteration;
+  if (int rc = coll_each(c, [&](brr_session *s) -> int {
+        Dev &d = s->d;
+        HIPCHK(launch_sweep_start(d, it, s->st));
+        if (int rc = rows_flagged(s, H_ROW_SHIFT | H_ROW_WRITE)) return rc;
+        if (s->order_mode == BRR_ORDER_BLOCKED) {
+          HIPCHK(launch_perm(d, it, 0, false, s->st));
+        } else if (s->order_mode == BRR_ORDER_REFERENCE) {
+          if (s->F > 0) {  // fixedI shuffled before markerI (BayesRv2Groups.cpp:216,227)
+            s->grand.shuffle(s->ref_forder);
+            HIPCHK(hipMemcpyAsync(d.forder, s->ref_forder.data(), (size_t)s->F * 4, hipMemcpyHostToDevice, s->st));
+          }
+          s->grand.shuffle(s->ref_order);
+          if (int rc = upload_order(s, s->ref_order)) return rc;
+        } else {
+          HIPCHK(launch_perm(d, it, 0, true, s->st));
+        }
+        return 0;
+      }))
+    return rc;
+  if (s0->order_mode == BRR_ORDER_REFERENCE)
+    if (int rc = coll_grams(c)) return rc;
+  if (int rc = coll_each(c, [](brr_session *s) -> int {
+        if (s->d.Xc) HIPCHK(launch_lut_order(s->d, s->st));
+        return 0;
+      }))
+    return rc;
+  if (s0->model == MODEL_GROUPS && s0->F > 0) {
+    const bool dev_perm = s0->order_mode == BRR_ORDER_BLOCKED;
+    for (int cf = 0; cf < s0->F; ++cf) {
+      if (int rc = coll_each(c, [&](brr_session *s) -> int {
+            HIPCHK(launch_fixed_row(s->d, it, cf, 0, dev_perm, s->st));
+            return 0;
+          }))
+        return rc;
+      if (int rc = coll_sum(c, [](brr_session *s) { return &s->d.sc->fx; }, 1)) return rc;
+      if (int rc = coll_each(c, [&](brr_session *s) -> int {
+            HIPCHK(launch_fixed_row(s->d, it, cf, 1, dev_perm, s->st));
+            return 0;
+          }))
+        return rc;
+    }
+  }
+  if (int rc = coll_each(c, [&](brr_session *s) -> int {
+        Dev &d = s->d;
+        d.sbase = s->sbase;
+        for (int k = 0; k < NPAR; ++k) d.gbase[k] = s->gbase[k];
+        d.abase = s->abase;
+        s->sbase += s->nb;
+        for (int k = 0; k < NPAR; ++k) s->gbase[k] += (s->nb + NPAR - 1 - k) / NPAR;
+        HIPCHK(launch_prep(d, it, s->st));
+        return 0;
+      }))
+    return rc;
+  // the marker loop: stream(b), the block's dots summed over the shards, solve(b - 1) (lag-1
+  // pipeline of the per-block kernels)
+  const int nb = s0->nb;
+  auto stream_b = [&](int b) {
+    return coll_each(c, [&](brr_session *s) -> int {
+      double *ebuf[2] = {s->d.eps, s->d.eps2};
+      HIPCHK(launch_stream(s->d, b, ebuf[b & 1], ebuf[(b + 1) & 1], s->st));
+      HIPCHK(launch_slab_total(s->d, b, s->st));
+      return 0;
+    });
+  };
+  auto solve_b = [&](int b) {
+    return coll_each(c, [&](brr_session *s) -> int {
+      Dev dp = s->d;
+      dp.NG = 1;  // the summed dots are in slab2 row 0
+      HIPCHK(launch_solve(dp, b, it, s->st));
+      return 0;
+    });
+  };
+  // instrumentation (one session): the whole marker loop between two events, per block position
+  const bool timed = c.ss.size() == 1 && s0->timing;
+  size_t ti = 0;
+  if (timed) {
+    ti = s0->ev_used;
+    hipEvent_t e0 = s0->ev();
+    (void)s0->ev();
+    HIPCHK(hipEventRecord(e0, s0->st));
+  }
+  for (int b = 0; b < nb; ++b) {
+    if (int rc = stream_b(b)) return rc;
+    if (int rc = coll_sum(c, [b](brr_session *s) { return s->d.slab2 + (b % NPAR) * s->d.slab2_stride; }, s0->B))
+      return rc;
+    if (b >= 1)
+      if (int rc = solve_b(b - 1)) return rc;
+  }
+  if (int rc = solve_b(nb - 1)) return rc;
+  if (timed) {
+    HIPCHK(hipEventRecord(s0->ev_pool[ti + 1], s0->st));
+    s0->ev_pairs.push_back({ti, 3});
+  }
+  if (int rc = coll_each(c, [&](brr_session *s) -> int {
+        Dev &d = s->d;
+        double *ebuf[2] = {d.eps, d.eps2};
+        const int sa = nb >= 2 ? (nb - 2) % NSLOT : -1, sb = (nb - 1) % NSLOT;
+        HIPCHK(launch_rows(d, H_ROW_PENDING | H_ROW_WRITE | H_ROW_REDUCE, nullptr, s->st, ebuf[nb & 1], sa, sb));
+        return 0;
+      }))
+    return rc;
+  if (int rc = coll_sum(c, sc_sums, 2)) return rc;
+  return coll_each(c, [&](brr_session *s) -> int {
+    const int mode = s->model == MODEL_HORSESHOE ? H_MR_HS : H_MR_BAYESR;
+    HIPCHK(launch_markers(s->d, mode, it, s->st));
+    HIPCHK(launch_hyper(s->d, it, s->d.stats, s->st));
+    s->iteration++;
+    if (s->timing) return collect_timing(s);
+    return 0;
+  });
+}
+
 }  // namespace
 
 // =======================================================================================
@@ -396,6 +661,7 @@ void brr_options_default(brr_options *o) {
   o->block_size = 0;  // automatic: 512 (V2, restart), 128 (Groups, Horseshoe)
   o->order_mode = BRR_ORDER_BLOCKED;
   o->shard_count = 1;
+  o->row_shard_count = 1;
 }
 
 const char *brr_last_error(void) { return g_last_error.c_str(); }
@@ -410,7 +676,23 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
                                 int64_t col_offset, int32_t K, int32_t groups, int64_t F,
                                 const brr_options *opt_in) {
   brr_options opt;
-  if (opt_in) opt = *opt_in; else brr_options_default(&opt);
+  brr_options_default(&opt);
+  if (opt_in) {
+    // an ABI-1 caller's struct ends before the row-shard fields: keep their defaults
+    if (opt_in->abi_version >= 2) opt = *opt_in;
+    else std::memcpy(&opt, opt_in, offsetof(brr_options, row_shard_rank));
+    opt.abi_version = BRR_ABI_VERSION;
+  }
+  if (opt.row_shard_count < 1) opt.row_shard_count = 1;
+  const bool rows = opt.row_shard_count > 1;
+  const int64_t N_total = opt.N_total > 0 ? opt.N_total : N;
+  if (rows) {
+    if (opt.shard_count > 1) { set_error("row shards and column shards cannot be combined"); return nullptr; }
+    if (opt.row_shard_count > GROUP_MAX) { set_error("row_shard_count > %d", GROUP_MAX); return nullptr; }
+    if (opt.row_shard_rank < 0 || opt.row_shard_rank >= opt.row_shard_count) { set_error("bad row_shard_rank"); return nullptr; }
+    if (opt.row_offset < 0 || opt.row_offset + N > N_total) { set_error("rows [row_offset, row_offset + N) outside N_total"); return nullptr; }
+    if (M_total != M || col_offset != 0) { set_error("a row shard holds every marker (M_total == M, col_offset 0)"); return nullptr; }
+  }
   if (model < 0 || model > 3) { set_error("bad model %d", model); return nullptr; }
   if (N < 1 || M < 1) { set_error("N and M must be >= 1"); return nullptr; }
   if (M_total < M) M_total = M;
@@ -464,10 +746,17 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   s->K = K; s->G = groups; s->F = (int)F; s->B = B; s->model = model;
   s->order_mode = opt.order_mode;
   s->shard = opt.shard_rank; s->nshard = opt.shard_count;
+  s->rshard = rows ? opt.row_shard_rank : 0; s->nrshard = opt.row_shard_count;
+  if (hipEventCreateWithFlags(&s->ev_x, hipEventDisableTiming) != hipSuccess) {
+    set_error("cannot create an event on HIP device %d", s->device);
+    delete s;
+    return nullptr;
+  }
   s->nb = (int)((M + B - 1) / B);
   s->NS = stats_size(groups, K);
   Dev &d = s->d;
   d.N = N; d.M = M; d.M_total = M_total; d.col_offset = col_offset;
+  d.Ntot = N_total; d.row_offset = rows ? opt.row_offset : 0;
   d.ld = (N + SROWS - 1) / SROWS * SROWS;  // every streaming row tile inside the allocation (zero rows)
   d.K = K; d.G = groups; d.F = (int)F; d.B = B; d.nb = s->nb; d.model = model;
   // streaming geometry: row tiles of SROWS rows (k_stream), NC = B/128 column chunks
@@ -590,7 +879,9 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     const bool lag2_pref = !s->x2bit && (model == MODEL_V2 || model == MODEL_RESTART);
     d.lag = (lag2_ok && (lg ? atoi(lg) >= 2 : lag2_pref)) ? 2 : 1;
     if (d.lag == 2 && lg && atoi(lg) >= 3 && s->nb >= 5) d.lag = 3;  // (diagnostics: BRR_LAG=3)
-    if (!(pb && pb[0] == '1') && !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused)) s->fused = FusedCfg{};
+    // row shards: the per-block kernels (the cross-shard sum of a block's dots sits between its
+    // streaming and its solve; the fused sweep's in-kernel hand-over is one device's)
+    if (rows || (pb && pb[0] == '1') || !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused)) s->fused = FusedCfg{};
     if (s->fused.nsg == 0) d.lag = 1;
     if ((d.lag >= 2 && (s->alloc(&d.xgram2, (int64_t)s->nb * B * B) || s->alloc(&d.xgram2T, (int64_t)s->nb * B * B))) ||
         (d.lag >= 3 && (s->alloc(&d.xgram3, (int64_t)s->nb * B * B) || s->alloc(&d.xgram3T, (int64_t)s->nb * B * B)))) {
@@ -827,7 +1118,7 @@ int brr_session_synthesize(brr_session *s, uint64_t ds, double h2, int64_t n_cau
   HIPCHK(hipStreamSynchronize(s->st));
   HIPCHK(hipMemcpy(s->synth_y.data(), dy, sizeof(double) * s->N, hipMemcpyDeviceToHost));
   (void)hipFree(dci); (void)hipFree(dcb); (void)hipFree(dy);
-  if (s->nshard > 1) return 0;  // Y needs every shard's genetic values: brr_session_synth_y
+  if (s->nshard > 1 || s->nrshard > 1) return 0;  // Y needs every shard's genetic values: brr_session_synth_y
   return brr_session_synth_y(s, s->synth_y.data(), ds, h2);
 }
 
@@ -839,19 +1130,22 @@ int brr_session_synth_partial_y(brr_session *s, double *out) {
 
 int brr_session_synth_y(brr_session *s, const double *g_sum, uint64_t ds, double h2) {
   if (!s || !g_sum) return -1;
-  std::vector<double> y(g_sum, g_sum + s->N);
+  // row shards: g_sum holds the genetic values of all N_total rows (row order); Y is
+  // standardised over the cohort and this shard keeps its rows
+  const int64_t NT = s->d.Ntot, r0 = s->d.row_offset;
+  std::vector<double> y(g_sum, g_sum + NT);
   const double se = std::sqrt(1.0 - h2);
   double mean = 0.0;
-  for (int64_t i = 0; i < s->N; ++i) {
+  for (int64_t i = 0; i < NT; ++i) {
     y[(size_t)i] += se * normal(ds, T_DATA_NOISE, (uint32_t)i, 0, 0);
     mean += y[(size_t)i];
   }
-  mean /= (double)s->N;
+  mean /= (double)NT;
   double ss = 0.0;
-  for (int64_t i = 0; i < s->N; ++i) ss += (y[(size_t)i] - mean) * (y[(size_t)i] - mean);
-  const double sd = s->N > 1 ? std::sqrt(ss / (double)(s->N - 1)) : 1.0;
+  for (int64_t i = 0; i < NT; ++i) ss += (y[(size_t)i] - mean) * (y[(size_t)i] - mean);
+  const double sd = NT > 1 ? std::sqrt(ss / (double)(NT - 1)) : 1.0;
   for (auto &v : y) v = (v - mean) / (sd > 0 ? sd : 1.0);  // Y = scale(y)
-  return brr_session_set_y(s, y.data());
+  return brr_session_set_y(s, y.data() + r0);
 }
 
 int brr_session_set_y(brr_session *s, const double *Y) {
@@ -928,50 +1222,18 @@ int brr_session_set_pi(brr_session *s, const double *pi) {
 
 int brr_session_init(brr_session *s, int32_t seed) {
   if (!s) return -1;
-  if (!s->have_x) { set_error("X not uploaded"); return -1; }
-  if (s->model != MODEL_RESTART && !s->have_y) { set_error("Y not set"); return -1; }
-  HIPCHK(hipSetDevice(s->device));
-  Dev &d = s->d;
-  d.seed = (uint64_t)(int64_t)seed;
-  // identity block layout -> Gram blocks and xsquared (BayesRv2.cpp:170)
-  HIPCHK(launch_perm(d, 0, s->shard, true, s->st));
-  HIPCHK(launch_gram(d, 0, d.gram, nullptr, s->st));
-  HIPCHK(launch_gram(d, 1, d.xgram, d.xgramT, s->st));  // cycle neighbours (b, b+1 mod nb)
-  if (d.lag >= 2) HIPCHK(launch_gram(d, 2, d.xgram2, d.xgram2T, s->st));  // (b, b+2 mod nb)
-  if (d.lag >= 3) HIPCHK(launch_gram(d, 3, d.xgram3, d.xgram3T, s->st));  // (b, b+3 mod nb)
-  HIPCHK(launch_xsq(d, s->st));
-  Scal sc{};
-  if (s->model == MODEL_RESTART) { sc.mu = s->mu0; sc.sigmaE = s->sigmaE0; }
-  if (s->model == MODEL_HORSESHOE) sc.c2 = d.hyp.c2_0;
-  HIPCHK(hipMemcpyAsync(d.sc, &sc, sizeof sc, hipMemcpyHostToDevice, s->st));
-  if (s->model != MODEL_RESTART) {
-    HIPCHK(hipMemsetAsync(d.beta, 0, sizeof(double) * s->M, s->st));
-    HIPCHK(hipMemsetAsync(d.comp, 0, sizeof(int) * s->M, s->st));
-  }
-  HIPCHK(hipMemsetAsync(d.sel, 0, s->M, s->st));
-  HIPCHK(hipMemsetAsync(d.alpha, 0, sizeof(double) * std::max(s->F, 1), s->st));
-  if (s->F > 0)  // identity fixed-effect order (IDENTITY mode; REFERENCE overwrites per sweep)
-    if (int rc = h2d(s, d.forder, s->ref_forder.data(), s->F)) return rc;
-  if (s->model == MODEL_HORSESHOE) {
-    std::vector<double> ones((size_t)s->M, 1.0);
-    if (int rc = h2d(s, d.lambda, ones.data(), s->M)) return rc;
-    if (int rc = h2d(s, d.hsv, ones.data(), s->M)) return rc;
-  }
-  if (int rc = rows_flagged(s, (s->model == MODEL_RESTART ? 0 : (H_ROW_INIT_Y | H_ROW_WRITE)) | H_ROW_REDUCE)) return rc;
-  if (s->model == MODEL_RESTART) {
-    HIPCHK(launch_markers(d, H_MR_COUNT_ALL, 0, s->st));
-    if (s->nshard > 1) { set_error("restart across shards needs summed counts: not supported"); return -1; }
-  }
-  HIPCHK(launch_hyper_init(d, d.stats, s->pi_given, s->st));
-  HIPCHK(hipStreamSynchronize(s->st));
-  s->iteration = 0;
-  s->initialized = true;
-  s->need_reduce = false;
-  return 0;
+  Coll c{{s}};
+  return coll_init(c, seed);
 }
 
 int brr_session_sweep(brr_session *s, int32_t n) {
   if (!s) return -1;
+  if (s->nrshard > 1) {
+    Coll c{{s}};
+    for (int r = 0; r < n; ++r)
+      if (int rc = coll_sweep_rows(c)) return rc;
+    return check_device_error(s);
+  }
   if (s->nshard > 1 && !s->comm) {
     set_error("sharded session without a communicator: brr_session_comm_init, or drive "
               "sweep_local / exchange / sweep_finish yourself");
@@ -1006,6 +1268,19 @@ int brr_comm_unique_id(void *out) {
 
 int brr_session_comm_init(brr_session *s, const void *unique_id, int32_t nranks, int32_t rank) {
   if (!s || !unique_id) return -1;
+  if (s->nrshard > 1) {  // row shards: only the communicator (no residual exchange buffers)
+    if (nranks != s->nrshard || rank != s->rshard) {
+      set_error("comm (%d ranks, rank %d) does not match the session's row shards (%d, %d)", nranks, rank,
+                s->nrshard, s->rshard);
+      return -1;
+    }
+    HIPCHK(hipSetDevice(s->device));
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof id);
+    ncclResult_t r = ncclCommInitRank(&s->comm, nranks, id, rank);
+    if (r != ncclSuccess) { set_error("ncclCommInitRank: %s", ncclGetErrorString(r)); s->comm = nullptr; return -2; }
+    return 0;
+  }
   if (nranks != s->nshard || rank != s->shard) {
     set_error("comm (%d ranks, rank %d) does not match the session's shards (%d, %d)", nranks, rank,
               s->nshard, s->shard);
@@ -1264,6 +1539,62 @@ int brr_session_timing(brr_session *s, double *stream_ms, int64_t *n_stream, dou
 }
 
 int64_t brr_session_block_size(brr_session *s) { return s ? s->B : -1; }
+
+// ---------------------------------------------------------------------------------------
+// In-process row-shard group
+struct brr_group {
+  Coll c;
+};
+
+brr_group *brr_group_create(brr_session *const *members, int32_t n) {
+  if (!members || n < 1 || n > GROUP_MAX) { set_error("brr_group_create: 1 .. %d members", GROUP_MAX); return nullptr; }
+  brr_group *g = new brr_group();
+  for (int i = 0; i < n; ++i) {
+    brr_session *s = members[i];
+    if (!s || s->nrshard != n || s->rshard != i) {
+      set_error("brr_group_create: member %d must be row shard %d of %d", i, i, n);
+      delete g;
+      return nullptr;
+    }
+    const brr_session *a = members[0];
+    if (s->model != a->model || s->M != a->M || s->B != a->B || s->K != a->K || s->G != a->G || s->F != a->F ||
+        s->order_mode != a->order_mode || s->d.Ntot != a->d.Ntot) {
+      set_error("brr_group_create: member %d differs from member 0 (model, M, B, K, groups, F, order, N_total)", i);
+      delete g;
+      return nullptr;
+    }
+    if (s->device != a->device) {  // members on other GPUs: the sum kernel runs on member 0's device
+      (void)hipSetDevice(a->device);
+      const hipError_t e = hipDeviceEnablePeerAccess(s->device, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+        set_error("brr_group_create: no peer access from device %d to %d", a->device, s->device);
+        delete g;
+        return nullptr;
+      }
+      (void)hipGetLastError();
+    }
+    g->c.ss.push_back(s);
+  }
+  return g;
+}
+
+int brr_group_init(brr_group *g, int32_t seed) {
+  if (!g) return -1;
+  return coll_init(g->c, seed);
+}
+
+int brr_group_sweep(brr_group *g, int32_t n) {
+  if (!g) return -1;
+  for (int r = 0; r < n; ++r)
+    if (int rc = coll_sweep_rows(g->c)) return rc;
+  for (brr_session *s : g->c.ss) {
+    HIPCHK(hipSetDevice(s->device));
+    if (int rc = check_device_error(s)) return rc;
+  }
+  return 0;
+}
+
+void brr_group_destroy(brr_group *g) { delete g; }
 
 int brr_session_synchronize(brr_session *s) {
   if (!s) return -1;

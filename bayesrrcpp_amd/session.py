@@ -28,13 +28,15 @@ class Session:
 
     def __init__(self, model, N, M, *, K=1, groups=1, F=0, M_total=None, col_offset=0,
                  device=0, block_size=0, order_mode=L.ORDER_BLOCKED, shard_rank=0,
-                 shard_count=1, verbose=0, log=None, x_storage=L.X_F32):
+                 shard_count=1, verbose=0, log=None, x_storage=L.X_F32, row_shard_rank=0,
+                 row_shard_count=1, row_offset=0, N_total=0):
         self._keep = []
         self.model, self.N, self.M, self.K, self.G, self.F = model, N, M, K, groups, F
         self.M_total = M if M_total is None else M_total
         self.col_offset = col_offset
+        self.row_offset, self.N_total = row_offset, (N_total or N)
         self.opt = L.options(device, block_size, order_mode, shard_rank, shard_count, verbose, log,
-                             x_storage)
+                             x_storage, row_shard_rank, row_shard_count, row_offset, N_total)
         self.h = L.lib().brr_session_create(model, N, M, self.M_total, col_offset, K, groups, F,
                                             C.byref(self.opt))
         if not self.h:
@@ -228,6 +230,41 @@ class Session:
     def close(self):
         if getattr(self, "h", None):
             L.lib().brr_session_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Group:
+    """Exact row shards driven in lock step from one process (brr_group_*).
+
+    members: Sessions created with row_shard_rank 0..n-1 / row_shard_count n (rows
+    [row_offset, row_offset + N) of an N_total-row cohort, every marker).  Data setters stay per
+    session; init and sweeps run through the group (the cross-shard sums happen on the device).
+    """
+
+    def __init__(self, members):
+        self.members = list(members)
+        arr = (C.c_void_p * len(self.members))(*[m.h for m in self.members])
+        self.h = L.lib().brr_group_create(arr, len(self.members))
+        if not self.h:
+            raise L.BrrError(f"brr_group_create failed: {L.last_error()}")
+
+    def init(self, seed=1):
+        L.check(L.lib().brr_group_init(self.h, seed), "group_init")
+        return self
+
+    def sweep(self, n=1):
+        L.check(L.lib().brr_group_sweep(self.h, n), "group_sweep")
+        return self
+
+    def close(self):
+        if getattr(self, "h", None):
+            L.lib().brr_group_destroy(self.h)
             self.h = None
 
     def __del__(self):

@@ -126,6 +126,9 @@ def parse():
     ap.add_argument("--cpu-sweeps", type=int, default=3)
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-roofline-events", action="store_true")
+    ap.add_argument("--shard", default="cols", choices=["cols", "rows"],
+                    help="N > 1: column shards with one residual all-reduce per sweep (north_star, SURVEY 8e; "
+                         "default) or exact row shards with an all-reduce of each block's dots (SURVEY 8f4)")
     ap.add_argument("--x-storage", default="f32", choices=["f32", "2bit"],
                     help="genotype storage on the device: dense f32 (the BASELINE configs) or 2-bit codes "
                          "+ per-column value tables (SURVEY 8f3; decoded values identical to f32)")
@@ -277,23 +280,36 @@ def main():
     model = {"v2": L.MODEL_V2, "groups": L.MODEL_GROUPS, "hs": L.MODEL_HORSESHOE}[cfg["model"]]
     Bsz = args.block_size or (128 if model in (L.MODEL_HORSESHOE, L.MODEL_GROUPS) else 512)  # = libbrr's automatic B
     G = cfg["groups"]
-    # contiguous block shards
-    nb = (P + Bsz - 1) // Bsz
-    b0, b1 = nb * rank // world, nb * (rank + 1) // world
-    c0, c1 = b0 * Bsz, min(P, b1 * Bsz)
-    Pl = c1 - c0
     K = 1 if model == L.MODEL_HORSESHOE else len(CVA) + 1
     F = 1 if model == L.MODEL_GROUPS else 0
     x2 = args.x_storage == "2bit"
-    s = B.Session(model, N, Pl, K=K, groups=G, F=F, M_total=P, col_offset=c0, device=local_rank,
-                  block_size=Bsz, order_mode=L.ORDER_BLOCKED, shard_rank=rank, shard_count=world,
-                  x_storage=L.X_2BIT if x2 else L.X_F32)
+    rows = args.shard == "rows" and world > 1
+    if rows:
+        # exact row shards: rows [r0, r1) of the cohort, every marker
+        r0, r1 = N * rank // world, N * (rank + 1) // world
+        c0, c1, Pl, Nl = 0, P, P, r1 - r0
+        s = B.Session(model, Nl, P, K=K, groups=G, F=F, device=local_rank, block_size=Bsz,
+                      order_mode=L.ORDER_BLOCKED, row_shard_rank=rank, row_shard_count=world, row_offset=r0,
+                      N_total=N, x_storage=L.X_2BIT if x2 else L.X_F32)
+    else:
+        # contiguous block shards
+        nb = (P + Bsz - 1) // Bsz
+        b0, b1 = nb * rank // world, nb * (rank + 1) // world
+        c0, c1 = b0 * Bsz, min(P, b1 * Bsz)
+        Pl, Nl = c1 - c0, N
+        s = B.Session(model, N, Pl, K=K, groups=G, F=F, M_total=P, col_offset=c0, device=local_rank,
+                      block_size=Bsz, order_mode=L.ORDER_BLOCKED, shard_rank=rank, shard_count=world,
+                      x_storage=L.X_2BIT if x2 else L.X_F32)
     # algorithmic bytes of one pass over this shard's genotypes (f32 values, or 2-bit codes + the
     # 16-B value table of every column)
-    x_bytes = (N * Pl / 4.0 + 16.0 * Pl) if x2 else 4.0 * N * Pl
+    x_bytes = (Nl * Pl / 4.0 + 16.0 * Pl) if x2 else 4.0 * Nl * Pl
     t_setup = time.perf_counter()
     s.synthesize(args.data_seed, 0.5, -1)
-    if world > 1:
+    if world > 1 and rows:
+        parts = [None] * world
+        dist.all_gather_object(parts, s.synth_partial_y())
+        s.synth_y(np.concatenate(parts), args.data_seed, 0.5)
+    elif world > 1:
         import torch
         g = torch.from_numpy(s.synth_partial_y())
         dist.all_reduce(g)
@@ -306,11 +322,11 @@ def main():
         s.set_bayesr(cva=np.tile(CVA, (G, 1)), gAssign=gA, **HYP)
         if F:
             s.set_fixed(np.zeros((N, F)))  # vignettes/BayesRR.Rmd:166: one all-zero column
-    s.init(args.seed)
-    if world > 1:
+    if world > 1:  # (row shards sum their Gram blocks inside init: the communicator comes first)
         uid = [comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         s.comm_init(uid[0], world, rank)
+    s.init(args.seed)
     s.synchronize()
     t_setup = time.perf_counter() - t_setup
 
@@ -361,10 +377,11 @@ def main():
         tm = s.timing()
         s.set_timing(False)
         nbl = (Pl + Bsz - 1) // Bsz
-        if fused:
+        if fused or rows:
             launches = max(1, tm["stream_launches"] // nbl)
             bytes_launch = x_bytes
-            kname = "k_sweep (fused marker loop: streaming + solver workgroups)"
+            kname = ("row-shard marker loop (per block: k_stream, k_slab_total, ncclAllReduce of the B dots, k_solve)"
+                     if rows else "k_sweep (fused marker loop: streaming + solver workgroups)")
         else:
             launches = max(1, tm["stream_launches"])
             bytes_launch = x_bytes * Bsz / Pl
@@ -431,7 +448,8 @@ def main():
                      + ("2-bit codes + f32 value tables" if x2 else "f32 X") + ", f64 arithmetic)"),
             "config": {"workload": cfg["workload"] + (" [2-bit genotype storage, SURVEY 8f3]" if x2 else ""),
                        "x_storage": args.x_storage, "N": N, "P": P, "K": K, "groups": G,
-                       "block_size": Bsz, "order": "blocked", "fused_stream_wg": int(s.scalar(104)), "code_cache": int(s.scalar(105)), "pipeline_lag": int(s.scalar(106)), "parallelism": f"column-shard x{world}",
+                       "block_size": Bsz, "order": "blocked", "fused_stream_wg": int(s.scalar(104)), "code_cache": int(s.scalar(105)), "pipeline_lag": int(s.scalar(106)),
+                       "parallelism": f"row-shard x{world} (exact)" if rows else f"column-shard x{world}",
                        "setup_s": round(t_setup, 2), "diag": diag},
             "roofline": roof, "cpu_baseline": cpu,
         }

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define BRR_ABI_VERSION 1
+#define BRR_ABI_VERSION 2
 
 enum brr_model { BRR_MODEL_V2 = 0, BRR_MODEL_GROUPS = 1, BRR_MODEL_RESTART = 2, BRR_MODEL_HORSESHOE = 3 };
 
@@ -70,6 +70,15 @@ typedef struct brr_options {
   int32_t x_storage;       /* enum brr_x_storage (default F32) */
   brr_log_fn log;          /* NULL = stderr */
   void *log_userdata;
+  /* exact row-sharded mode (ABI 2): this session holds rows
+   * [row_offset, row_offset + N) of an N_total-row cohort and ALL markers; per marker block the
+   * partial dots x_j . eps are summed across the row shards before the (replicated, identical)
+   * block solve, so every shard runs the single-GPU chain exactly.  Exchanges go through RCCL
+   * (brr_session_comm_init, one process per GPU) or an in-process brr_group. */
+  int32_t row_shard_rank;  /* default 0 */
+  int32_t row_shard_count; /* default 1 (no row sharding) */
+  int64_t row_offset;      /* first global row of this shard */
+  int64_t N_total;         /* rows of the whole cohort (0 = N) */
 } brr_options;
 
 void brr_options_default(brr_options *opt);
@@ -129,7 +138,10 @@ int brr_session_upload_bed(brr_session *s, const uint8_t *bed, int64_t bytes_per
 int brr_session_synthesize(brr_session *s, uint64_t data_seed, double h2, int64_t n_causal);
 /* sharded synthetic Y: Y = scale(sum over shards of X_c beta_c + noise).  Each process reads
  * its shard's genetic values, the caller sums them across processes, then every process
- * calls brr_session_synth_y with the sum (identical Y everywhere). */
+ * calls brr_session_synth_y with the sum (identical Y everywhere).  Row shards: every shard
+ * holds all markers, so its partial values are final for its rows; the caller concatenates them
+ * in row order (N_total values) and every shard calls brr_session_synth_y with that vector (Y is
+ * standardised over all N_total rows; each shard keeps its own rows). */
 int brr_session_synth_partial_y(brr_session *s, double *out /* N */);
 int brr_session_synth_y(brr_session *s, const double *genetic_sum /* N */, uint64_t data_seed,
                         double h2);
@@ -172,9 +184,24 @@ int brr_session_sweep_finish(brr_session *s);
 /* native multi-GPU: RCCL over xGMI, one process per GPU.  Rank 0 creates the 128-byte id,
  * the caller broadcasts it (MPI, a file, torch.distributed/gloo ...), every rank calls
  * brr_session_comm_init; brr_session_sweep then runs local sweep -> ncclAllReduce(sum) of
- * the exchange buffers on the session stream -> finish, with no host round trip. */
+ * the exchange buffers on the session stream -> finish, with no host round trip.
+ * Row-sharded sessions (row_shard_count > 1) take nranks = row_shard_count, rank =
+ * row_shard_rank and must call it BEFORE brr_session_init (the Gram blocks are summed there);
+ * their sweeps then all-reduce B partial dots per marker block (exact chain). */
 int brr_comm_unique_id(void *out /* 128 bytes */);
 int brr_session_comm_init(brr_session *s, const void *unique_id, int32_t nranks, int32_t rank);
+
+/* exact row shards in ONE process: the sessions (created with row_shard_rank
+ * 0..n-1, same model / M / options, on one device or on peer-accessible devices) are driven in
+ * lock step; the per-block partial dots, the residual sums, the fixed-effect dots and, at init,
+ * the Gram blocks are summed across the members on the device (rank order) instead of by RCCL.
+ * Setters (upload, set_y, set_bayesr ...) stay per session; init and sweeps go through the group.
+ * The group borrows the sessions (destroy the group first). */
+typedef struct brr_group brr_group;
+brr_group *brr_group_create(brr_session *const *members, int32_t n);
+int brr_group_init(brr_group *g, int32_t seed);
+int brr_group_sweep(brr_group *g, int32_t n);
+void brr_group_destroy(brr_group *g);
 
 /* state read-back (host buffers) */
 enum brr_scalar { BRR_MU = 0, BRR_SIGMAE, BRR_SIGMAG, BRR_SIGMAF, BRR_TAU, BRR_ETA, BRR_C2,

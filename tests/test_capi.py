@@ -84,8 +84,22 @@ def test_header_compiles_as_c(tmp_path):
     assert r.returncode == 0, r.stderr
 
 
-def test_options_struct_layout(brr):
+def test_options_struct_layout(brr, tmp_path):
+    # the ctypes mirror has the C compiler's layout of brr_options (ABI 2: row-shard fields)
     from bayesrrcpp_amd import _lib
     o = _lib.options()
-    assert C.sizeof(_lib.Options) == 8 * 4 + 8 + 8
-    assert o.abi_version == _lib.ABI_VERSION == 1
+    assert o.abi_version == _lib.ABI_VERSION == 2
+    assert o.row_shard_count == 1 and o.row_shard_rank == 0 and o.N_total == 0
+    src = tmp_path / "lay.c"
+    fields = [f[0] for f in _lib.Options._fields_]
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "brr.h"\nint main(void){'
+                   'printf("%zu", sizeof(brr_options));'
+                   + "".join(f'printf(" %zu", offsetof(brr_options, {f}));' for f in fields)
+                   + 'return 0;}\n')
+    exe = tmp_path / "lay"
+    r = subprocess.run(["gcc", "-std=c99", f"-I{REPO}/include", str(src), "-o", str(exe)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    assert got[0] == C.sizeof(_lib.Options)
+    assert got[1:] == [getattr(_lib.Options, f).offset for f in fields]
