@@ -2484,12 +2484,18 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
                                                         int nred, int ccache) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_np[2];
-  // residency census: every workgroup must be running before any waits on another
+  __shared__ int s_ok;
+  // residency census: every workgroup must be running before any waits on another.  (The
+  // cooperative launch guarantees it; the census is the defence.)  A workgroup whose census
+  // timed out -- or that arrives after another one's did -- leaves before touching any state,
+  // so a failed census costs one sweep's marker loop, never the chain's consistency.
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(d.sync + SY_ARRIVE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     wait_geq(d.sync + SY_ARRIVE, d.abase + nsg + 1 + nred, d.sync, 5);
+    s_ok = ld_sc1_int(d.sync + SY_ERR) == 0;
   }
   __syncthreads();
+  if (!s_ok) return;
   if (blockIdx.x == 0) {
     solver_role<HS, B>(d, it, nslot, smem);
   } else if ((int)blockIdx.x > nsg) {
@@ -2883,24 +2889,18 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   return true;
 }
 
+// A cooperative launch: the runtime starts the grid only when every workgroup can be resident
+// at once (or fails the launch), which the in-kernel hand-over relies on.  BRR_TEST_CENSUS_EXTRA
+// (tests) raises the census target above the grid to exercise the failed-census exit.
 hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipStream_t st) {
-  const bool hs = d.model == MODEL_HORSESHOE, xf = d.Xc != nullptr;
-  const dim3 grid((unsigned)(c.nsg + 1 + c.nred)), blk(SWEEP_NT);
-#define BRR_SWEEP_LAUNCH(HSV, BV)                                                                                  \
-  do {                                                                                                             \
-    if (xf) hipLaunchKernelGGL((k_sweep<HSV, BV, 1>), grid, blk, c.lds, st, d, it, c.nslot, c.nsg, c.rpw, c.npass, \
-                               c.nred, c.ccache);                                                                  \
-    else hipLaunchKernelGGL((k_sweep<HSV, BV, 0>), grid, blk, c.lds, st, d, it, c.nslot, c.nsg, c.rpw, c.npass,    \
-                            c.nred, 0);                                                                            \
-  } while (0)
-  switch (d.B) {
-    case 128: if (hs) BRR_SWEEP_LAUNCH(true, 128); else BRR_SWEEP_LAUNCH(false, 128); break;
-    case 256: if (hs) BRR_SWEEP_LAUNCH(true, 256); else BRR_SWEEP_LAUNCH(false, 256); break;
-    case 512: if (hs) BRR_SWEEP_LAUNCH(true, 512); else BRR_SWEEP_LAUNCH(false, 512); break;
-    default: return hipErrorInvalidValue;
-  }
-#undef BRR_SWEEP_LAUNCH
-  return hipGetLastError();
+  const void *fn = sweep_kernel(d.model, d.B, d.Xc != nullptr);
+  if (!fn) return hipErrorInvalidValue;
+  Dev dd = d;
+  if (const char *ex = getenv("BRR_TEST_CENSUS_EXTRA")) dd.abase += atoi(ex);
+  int nslot = c.nslot, nsg = c.nsg, rpw = c.rpw, npass = c.npass, nred = c.nred, cc = d.Xc ? c.ccache : 0;
+  void *args[] = {&dd, &it, &nslot, &nsg, &rpw, &npass, &nred, &cc};
+  return hipLaunchCooperativeKernel(fn, dim3((unsigned)(c.nsg + 1 + c.nred)), dim3(SWEEP_NT), args,
+                                    (unsigned)c.lds, st);
 }
 
 hipError_t launch_prep(const Dev &d, uint32_t it, hipStream_t st) {

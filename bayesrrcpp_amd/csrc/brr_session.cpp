@@ -236,6 +236,22 @@ int check_device_error(brr_session *s) {
                   ((double)ts[4] - ts[0]) / 100.0, ((double)ts[5] - ts[0]) / 100.0, ((double)ts[6] - ts[0]) / 100.0,
                   ((double)ts[7] - ts[0]) / 100.0);
     set_error("%s%s", msg.c_str(), buf);
+    // the error is reported once: clear the flag so the session can go on.  A failed residency
+    // census (site 5) left the sweep's marker loop undone but the state consistent (every
+    // workgroup exited before touching it): later sweeps use the per-block kernels.
+    HIPCHK(hipMemset(s->d.sync + SY_ERR, 0, sizeof(int) * 5));
+    if (sy[SY_ERR + 1] == 5 && s->fused.nsg > 0) {
+      s->fused = FusedCfg{};
+      s->d.lag = 1;
+      // the hand-over counters are cumulative epochs of one pipeline geometry (and the failed
+      // sweep advanced none of them): start every epoch again from zero
+      const int NC = s->B >= 128 ? s->B / 128 : 1;
+      HIPCHK(hipMemset(s->d.sync, 0, sizeof(int) * SY_WORDS));
+      HIPCHK(hipMemset(s->d.cnt1, 0, sizeof(int) * NPAR * s->d.NG * NC));
+      s->sbase = s->abase = 0;
+      for (int k = 0; k < NPAR; ++k) s->gbase[k] = 0;
+      s->log("libbrr: fused sweep could not be made resident; using the per-block kernels\n");
+    }
     return -3;
   }
   return 0;

@@ -528,3 +528,27 @@ def test_f64_x_not_f32_representable(brr, oracle_mod, require_gpu):
     if same.all():
         assert _rel(s.vector(L.BETA), o64.vector(O.V_BETA)) < 1e-5
         assert _rel([s.scalar(L.SIGMAE)], [o64.scalar(O.S_SIGMAE)]) < 1e-5
+
+
+def test_failed_census_exits_cleanly(brr, oracle_mod, require_gpu, monkeypatch):
+    """A fused sweep whose residency census fails (forced: target above the grid) returns the
+    protocol error without touching the chain's state; the session then goes on with the
+    per-block kernels and keeps eps = Y - mu - X beta."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P = 2000, 1024
+    X, Y, _ = _cohort(O, N, P, n_causal=30)
+    s, _ = _make(brr, O, L.MODEL_V2, X, Y, 0, B=128)
+    s.sweep(2)
+    assert s.scalar(104) > 0  # fused
+    beta0, eps0 = s.vector(L.BETA), s.vector(L.EPS)
+    monkeypatch.setenv("BRR_TEST_CENSUS_EXTRA", "100000")
+    with pytest.raises(L.BrrError, match="site 5"):
+        s.sweep(1)
+    monkeypatch.delenv("BRR_TEST_CENSUS_EXTRA")
+    assert np.array_equal(s.vector(L.BETA), beta0)  # the marker loop never ran
+    assert s.scalar(104) == 0                       # per-block kernels from now on
+    s.sweep(3)
+    resid = Y - s.scalar(L.MU) - X.astype(np.float64) @ s.vector(L.BETA)
+    assert _rel(s.vector(L.EPS), resid) < 1e-9
+    assert not np.array_equal(s.vector(L.EPS), eps0)
