@@ -53,6 +53,7 @@ EXPORTED = [
     "brr_session_set_timing", "brr_session_timing", "brr_session_block_size",
     "brr_session_synchronize", "brr_session_linear_predictor",
     "brr_group_create", "brr_group_init", "brr_group_sweep", "brr_group_destroy",
+    "brr_session_output_open", "brr_session_output_sample", "brr_session_output_close",
 ]
 
 _lib = None
@@ -133,6 +134,10 @@ def lib():
     L.brr_group_init.argtypes = [vp, C.c_int32]
     L.brr_group_sweep.argtypes = [vp, C.c_int32]
     L.brr_group_destroy.argtypes = [vp]
+    L.brr_session_output_open.argtypes = [vp, C.c_char_p, C.c_int32, C.c_int64, C.c_int64, C.c_int32, C.c_int64,
+                                          C.c_int32, C.c_int32]
+    L.brr_session_output_sample.argtypes = [vp, C.c_int32]
+    L.brr_session_output_close.argtypes = [vp, C.POINTER(C.c_int32)]
     _lib = L
     return L
 

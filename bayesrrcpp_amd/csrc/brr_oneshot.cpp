@@ -9,9 +9,13 @@
 // before returning and HorseshoeR writes every kept sample.
 #include <hip/hip_runtime.h>
 
+#include <charconv>
 #include <chrono>
+#include <map>
+#include <memory>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -20,6 +24,7 @@
 #include <vector>
 
 #include "../../include/brr.h"
+#include "brr_sample.hpp"
 
 namespace {
 
@@ -31,16 +36,20 @@ struct Log {
   }
 };
 
+// The writer thread: header strings and sample slots (brr_sample.hpp) in order.  A sample row is
+// formatted straight from the slot's pinned host copy, then the slot is released to the sampler.
 class CsvWriter {
  public:
   explicit CsvWriter(FILE *f) : f_(f), th_([this] { run(); }) {}
   ~CsvWriter() { close(); }
-  void header(const std::string &h) { std::lock_guard<std::mutex> lk(mu_); q_.push_back({true, h, {}}); cv_.notify_one(); }
-  void row(std::vector<double> &&v) {
-    std::lock_guard<std::mutex> lk(mu_);
-    q_.push_back({false, std::string(), std::move(v)});
-    cv_.notify_one();
+  void header(const std::string &h) { push({true, h, -1, 0}); }
+  // the row layout of the session's model (BayesRv2.cpp:261-272, BayesRv2Groups.cpp:317,
+  // BRv2Grstart.cpp:267, HorseshoeR.cpp:258)
+  void bind(brr_session *s, int model, int64_t N, int64_t M, int G, int64_t F) {
+    s_ = s; model_ = model; N_ = N; M_ = M; G_ = G; F_ = F;
   }
+  void sample(int slot, int iteration) { push({false, std::string(), slot, iteration}); }
+  int error() const { return err_; }
   void close() {
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -52,10 +61,47 @@ class CsvWriter {
   }
 
  private:
-  struct Item { bool is_header; std::string h; std::vector<double> v; };
+  struct Item { bool is_header; std::string h; int slot; int iteration; };
+  void push(Item &&it) {
+    std::lock_guard<std::mutex> lk(mu_);
+    q_.push_back(std::move(it));
+    cv_.notify_one();
+  }
+  void put(double v) {
+    if (!first_) buf_ += ", ";
+    first_ = false;
+    // %g (6 significant digits, Eigen StreamPrecision, BayesRv2.cpp:72) without printf's
+    // locale and parsing overhead: std::to_chars with the general format and precision 6 is
+    // specified as printf("%.6g")
+    const auto res = std::to_chars(num_, num_ + sizeof num_, v, std::chars_format::general, 6);
+    buf_.append(num_, (size_t)(res.ptr - num_));
+  }
+  void put(const double *v, int64_t n) { for (int64_t i = 0; i < n; ++i) put(v[i]); }
+  void format(const brr::SampleView &v, int iteration) {
+    buf_.clear();
+    first_ = true;
+    put((double)iteration);
+    put(v.sc->mu);
+    put(v.beta, M_);
+    put(v.sc->sigmaE);
+    if (model_ == BRR_MODEL_HORSESHOE) {
+      put(v.sc->tau);
+      put(v.lam, M_);
+      put(v.eps, N_);
+      put(0.0);  // sample has 2M+4+N slots, 2M+N+3 values (HorseshoeR.cpp:157,258)
+    } else {
+      if (model_ == BRR_MODEL_V2) put(v.sgg[0]);
+      for (int64_t i = 0; i < M_; ++i) put((double)v.comp[i]);
+      if (model_ != BRR_MODEL_V2) put(v.sgg, G_);
+      put(v.eps, N_);
+      if (model_ == BRR_MODEL_GROUPS) {
+        put(v.alpha, F_);
+        put(v.sc->sigmaF);
+      }
+    }
+    buf_ += '\n';
+  }
   void run() {
-    std::string buf;
-    char num[40];
     for (;;) {
       Item it;
       {
@@ -66,17 +112,24 @@ class CsvWriter {
         q_.pop_front();
       }
       if (it.is_header) { fputs(it.h.c_str(), f_); continue; }
-      buf.clear();
-      for (size_t i = 0; i < it.v.size(); ++i) {
-        if (i) buf += ", ";
-        int n = snprintf(num, sizeof num, "%g", it.v[i]);
-        buf.append(num, (size_t)n);
+      brr::SampleView v;
+      if (brr::sample_ring_wait(s_, it.slot, &v) != 0) {
+        err_ = -2;
+      } else {
+        format(v, it.iteration);
+        fwrite(buf_.data(), 1, buf_.size(), f_);
       }
-      buf += '\n';
-      fwrite(buf.data(), 1, buf.size(), f_);
+      brr::sample_ring_release(s_, it.slot);
     }
   }
   FILE *f_;
+  brr_session *s_ = nullptr;
+  int model_ = 0, G_ = 1;
+  int64_t N_ = 0, M_ = 0, F_ = 0;
+  std::string buf_;
+  char num_[40];
+  bool first_ = true;
+  int err_ = 0;
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<Item> q_;
@@ -153,12 +206,14 @@ int fail(brr_session *s, const Log &log, int rc) {
   return rc < 0 ? rc : -1;
 }
 
-// the reference's sweep loop with sample emission (BayesRv2.cpp:171-278)
+// the reference's sweep loop with sample emission (BayesRv2.cpp:171-278).  Kept iterations go
+// through the session's sample ring: a device snapshot, an asynchronous copy to pinned memory
+// and the writer thread, so the sampler never waits for a row's D2H copy or its formatting
+// unless the writer is BRR_SAMPLE_RING (default 4) rows behind.
 int run_chain(brr_session *s, const Run &r, CsvWriter *w) {
-  const int64_t N = r.N, M = r.M;
-  const int G = r.G;
-  std::vector<double> beta((size_t)M), comp((size_t)M), eps((size_t)N), sgg((size_t)G), alpha((size_t)std::max<int64_t>(r.F, 1)),
-      lam((size_t)M);
+  const char *rd = getenv("BRR_SAMPLE_RING");
+  if (int rc = brr::sample_ring_open(s, rd ? atoi(rd) : 4)) return rc;
+  w->bind(s, r.model, r.N, r.M, r.G, r.F);
   const auto t1 = std::chrono::steady_clock::now();
   const int every = r.max_it / 10;  // (int)std::ceil(max_iterations/10): integer division
   for (int it = 0; it < r.max_it; ++it) {
@@ -176,43 +231,9 @@ int run_chain(brr_session *s, const Run &r, CsvWriter *w) {
     }
     if (int rc = brr_session_sweep(s, 1)) return rc;
     if (it >= r.burn_in && it % r.thin == 0) {
-      double mu = 0, se = 0, sg = 0, tau = 0, sf = 0;
-      if (brr_session_get_scalar(s, BRR_MU, &mu) || brr_session_get_scalar(s, BRR_SIGMAE, &se)) return -2;
-      if (brr_session_get_vector(s, BRR_BETA, beta.data()) < 0 || brr_session_get_vector(s, BRR_EPS, eps.data()) < 0) return -2;
-      std::vector<double> row;
-      row.reserve((size_t)(2 * M + N + G + r.F + 8));
-      row.push_back(it);
-      row.push_back(mu);
-      row.insert(row.end(), beta.begin(), beta.end());
-      row.push_back(se);
-      if (r.model == BRR_MODEL_HORSESHOE) {
-        brr_session_get_scalar(s, BRR_TAU, &tau);
-        if (brr_session_get_vector(s, BRR_LAMBDA, lam.data()) < 0) return -2;
-        row.push_back(tau);
-        row.insert(row.end(), lam.begin(), lam.end());
-        row.insert(row.end(), eps.begin(), eps.end());
-        row.push_back(0.0);  // sample has 2M+4+N slots, 2M+N+3 values (HorseshoeR.cpp:157,258)
-      } else {
-        if (brr_session_get_vector(s, BRR_COMP, comp.data()) < 0) return -2;
-        if (r.model == BRR_MODEL_V2) {
-          brr_session_get_scalar(s, BRR_SIGMAG, &sg);
-          row.push_back(sg);
-          row.insert(row.end(), comp.begin(), comp.end());
-          row.insert(row.end(), eps.begin(), eps.end());
-        } else {
-          if (brr_session_get_vector(s, BRR_SIGMAGG, sgg.data()) < 0) return -2;
-          row.insert(row.end(), comp.begin(), comp.end());
-          row.insert(row.end(), sgg.begin(), sgg.end());
-          row.insert(row.end(), eps.begin(), eps.end());
-          if (r.model == BRR_MODEL_GROUPS) {
-            if (r.F > 0 && brr_session_get_vector(s, BRR_ALPHA, alpha.data()) < 0) return -2;
-            row.insert(row.end(), alpha.begin(), alpha.begin() + r.F);
-            brr_session_get_scalar(s, BRR_SIGMAF, &sf);
-            row.push_back(sf);
-          }
-        }
-      }
-      w->row(std::move(row));
+      int slot = -1;
+      if (int rc = brr::sample_ring_push(s, &slot)) return rc;
+      w->sample(slot, it);
     }
   }
   brr_session_synchronize(s);
@@ -257,6 +278,7 @@ int brr_BayesRSamplerV2(const char *outputFile, int seed, int max_iterations, in
   if (!rc) rc = run_chain(s, r, &w);
   w.close();
   fclose(f);
+  if (!rc && w.error()) rc = w.error();
   if (rc) return fail(s, log, rc);
   brr_session_destroy(s);
   return 0;
@@ -291,6 +313,7 @@ int brr_BayesRSamplerV2Groups(const char *outputFile, int seed, int max_iteratio
   if (!rc) rc = run_chain(s, r, &w);
   w.close();
   fclose(f);
+  if (!rc && w.error()) rc = w.error();
   if (rc) return fail(s, log, rc);
   brr_session_destroy(s);
   return 0;
@@ -323,6 +346,7 @@ int brr_BRV2Grstart(const char *outputFile, int seed, int max_iterations, int bu
   if (!rc) rc = run_chain(s, r, &w);
   w.close();
   fclose(f);
+  if (!rc && w.error()) rc = w.error();
   if (rc) return fail(s, log, rc);
   brr_session_destroy(s);
   return 0;
@@ -360,9 +384,73 @@ int brr_HorseshoeR(const char *outputFile, int seed, int max_iterations, int bur
   if (!rc) rc = run_chain(s, r, &w);
   w.close();
   fclose(f);
+  if (!rc && w.error()) rc = w.error();
   if (rc) return fail(s, log, rc);
   brr_session_destroy(s);
   return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Sample output of a session: the one-shots' CSV pipeline for callers that drive
+// sweeps themselves (bench.py's output-on run).  One writer per session, kept here.
+namespace {
+struct Output {
+  FILE *f = nullptr;
+  std::unique_ptr<CsvWriter> w;
+};
+std::mutex g_out_mu;
+std::map<brr_session *, std::unique_ptr<Output>> g_out;
+}  // namespace
+
+int brr_session_output_open(brr_session *s, const char *path, int32_t model, int64_t N, int64_t M, int32_t groups,
+                            int64_t F, int32_t header, int32_t ring_depth) {
+  if (!s || !path) return -1;
+  std::lock_guard<std::mutex> lk(g_out_mu);
+  if (g_out.count(s)) return -1;
+  auto o = std::make_unique<Output>();
+  o->f = fopen(path, "w");
+  if (!o->f) return -3;
+  if (int rc = brr::sample_ring_open(s, ring_depth)) { fclose(o->f); return rc; }
+  o->w = std::make_unique<CsvWriter>(o->f);
+  if (header) {
+    if (model == BRR_MODEL_V2) o->w->header(hdr_v2(M, N));
+    else if (model == BRR_MODEL_GROUPS) o->w->header(hdr_groups(M, N, groups, F));
+    else if (model == BRR_MODEL_HORSESHOE) o->w->header(hdr_hs(M, N));
+  }
+  o->w->bind(s, model, N, M, groups, F);
+  g_out[s] = std::move(o);
+  return 0;
+}
+
+int brr_session_output_sample(brr_session *s, int32_t iteration) {
+  Output *o = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_out_mu);
+    auto it = g_out.find(s);
+    if (it == g_out.end()) return -1;
+    o = it->second.get();
+  }
+  int slot = -1;
+  if (int rc = brr::sample_ring_push(s, &slot)) return rc;
+  o->w->sample(slot, iteration);
+  return 0;
+}
+
+int brr_session_output_close(brr_session *s, int32_t *max_rows_in_flight) {
+  std::unique_ptr<Output> o;
+  {
+    std::lock_guard<std::mutex> lk(g_out_mu);
+    auto it = g_out.find(s);
+    if (it == g_out.end()) return -1;
+    o = std::move(it->second);
+    g_out.erase(it);
+  }
+  o->w->close();
+  const int err = o->w->error();
+  fclose(o->f);
+  if (max_rows_in_flight) *max_rows_in_flight = brr::sample_ring_max_in_use(s);
+  brr::sample_ring_close(s);
+  return err;
 }
 
 }  // extern "C"

@@ -28,6 +28,7 @@
 #include "brr_device.hpp"
 #include "brr_launch.hpp"
 #include "brr_rng.hpp"
+#include "brr_sample.hpp"
 
 using namespace brr;
 
@@ -116,6 +117,19 @@ int dalloc(T **p, int64_t n) {
 
 }  // namespace
 
+// sample output ring (brr_sample.hpp)
+struct SampleRing {
+  int depth = 0;
+  hipStream_t cst = nullptr;  // copy stream (device -> pinned host)
+  size_t bytes = 0, o_beta = 0, o_eps = 0, o_lam = 0, o_sgg = 0, o_alpha = 0, o_comp = 0;
+  std::vector<char *> dbuf, hbuf;
+  std::vector<hipEvent_t> ev_snap, ev_host;
+  std::vector<char> busy;
+  int next = 0, in_use = 0, max_in_use = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+};
+
 struct brr_session {
   brr_options opt;
   Logger log;
@@ -149,6 +163,7 @@ struct brr_session {
   double t_stream = 0, t_solve = 0, t_solve_sweep = 0;
   int64_t n_stream = 0, n_solve = 0, n_solve_sweep = 0;
   std::vector<void *> allocs;
+  SampleRing ring;
 
   template <class T>
   int alloc(T **p, int64_t n) {
@@ -158,6 +173,7 @@ struct brr_session {
   }
   ~brr_session() {
     if (st) (void)hipStreamSynchronize(st);
+    brr::sample_ring_close(this);
     if (comm) (void)ncclCommDestroy(comm);
     for (void *p : allocs) (void)hipFree(p);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
@@ -1620,3 +1636,117 @@ int brr_session_synchronize(brr_session *s) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------
+// Sample output ring (brr_sample.hpp)
+namespace brr {
+
+int sample_ring_open(brr_session *s, int depth) {
+  sample_ring_close(s);
+  SampleRing &r = s->ring;
+  if (depth < 1) depth = 1;
+  HIPCHK(hipSetDevice(s->device));
+  auto al = [](size_t b) { return (b + 255) / 256 * 256; };
+  size_t o = al(sizeof(Scal));
+  r.o_beta = o; o += al(8 * (size_t)s->M);
+  r.o_eps = o; o += al(8 * (size_t)s->N);
+  r.o_lam = o; o += s->model == MODEL_HORSESHOE ? al(8 * (size_t)s->M) : 0;
+  r.o_sgg = o; o += al(8 * (size_t)s->G);
+  r.o_alpha = o; o += al(8 * (size_t)std::max(s->F, 1));
+  r.o_comp = o; o += al(4 * (size_t)s->M);
+  r.bytes = o;
+  HIPCHK(hipStreamCreateWithFlags(&r.cst, hipStreamNonBlocking));
+  r.depth = depth;
+  r.dbuf.assign(depth, nullptr);
+  r.hbuf.assign(depth, nullptr);
+  r.ev_snap.assign(depth, nullptr);
+  r.ev_host.assign(depth, nullptr);
+  r.busy.assign(depth, 0);
+  r.next = r.in_use = r.max_in_use = 0;
+  for (int i = 0; i < depth; ++i) {
+    HIPCHK(hipMalloc((void **)&r.dbuf[i], r.bytes));
+    HIPCHK(hipHostMalloc((void **)&r.hbuf[i], r.bytes, hipHostMallocDefault));
+    HIPCHK(hipEventCreateWithFlags(&r.ev_snap[i], hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&r.ev_host[i], hipEventDisableTiming));
+  }
+  return 0;
+}
+
+int sample_ring_push(brr_session *s, int *slot_out) {
+  SampleRing &r = s->ring;
+  if (r.depth == 0) { set_error("sample ring not open"); return -1; }
+  int slot;
+  {
+    std::unique_lock<std::mutex> lk(r.mu);
+    r.cv.wait(lk, [&] { return !r.busy[r.next]; });  // back-pressure: the writer is r.depth rows behind
+    slot = r.next;
+    r.busy[slot] = 1;
+    r.next = (r.next + 1) % r.depth;
+    r.max_in_use = std::max(r.max_in_use, ++r.in_use);
+  }
+  HIPCHK(hipSetDevice(s->device));
+  if (int rc = ensure_reduced(s)) return rc;
+  char *d = r.dbuf[slot];
+  const Dev &dv = s->d;
+  auto cp = [&](size_t off, const void *src, size_t n) {
+    return n ? hipMemcpyAsync(d + off, src, n, hipMemcpyDeviceToDevice, s->st) : hipSuccess;
+  };
+  HIPCHK(cp(0, dv.sc, sizeof(Scal)));
+  HIPCHK(cp(r.o_beta, dv.beta, 8 * (size_t)s->M));
+  HIPCHK(cp(r.o_eps, dv.eps, 8 * (size_t)s->N));
+  if (s->model == MODEL_HORSESHOE) HIPCHK(cp(r.o_lam, dv.lambda, 8 * (size_t)s->M));
+  HIPCHK(cp(r.o_sgg, dv.sigmaGG, 8 * (size_t)s->G));
+  if (s->F > 0) HIPCHK(cp(r.o_alpha, dv.alpha, 8 * (size_t)s->F));
+  HIPCHK(cp(r.o_comp, dv.comp, 4 * (size_t)s->M));
+  HIPCHK(hipEventRecord(r.ev_snap[slot], s->st));
+  HIPCHK(hipStreamWaitEvent(r.cst, r.ev_snap[slot], 0));
+  HIPCHK(hipMemcpyAsync(r.hbuf[slot], d, r.bytes, hipMemcpyDeviceToHost, r.cst));
+  HIPCHK(hipEventRecord(r.ev_host[slot], r.cst));
+  *slot_out = slot;
+  return 0;
+}
+
+int sample_ring_wait(brr_session *s, int slot, SampleView *v) {
+  SampleRing &r = s->ring;
+  HIPCHK(hipEventSynchronize(r.ev_host[slot]));
+  const char *h = r.hbuf[slot];
+  v->sc = reinterpret_cast<const Scal *>(h);
+  v->beta = reinterpret_cast<const double *>(h + r.o_beta);
+  v->eps = reinterpret_cast<const double *>(h + r.o_eps);
+  v->lam = reinterpret_cast<const double *>(h + r.o_lam);
+  v->sgg = reinterpret_cast<const double *>(h + r.o_sgg);
+  v->alpha = reinterpret_cast<const double *>(h + r.o_alpha);
+  v->comp = reinterpret_cast<const int32_t *>(h + r.o_comp);
+  return 0;
+}
+
+void sample_ring_release(brr_session *s, int slot) {
+  SampleRing &r = s->ring;
+  {
+    std::lock_guard<std::mutex> lk(r.mu);
+    r.busy[slot] = 0;
+    --r.in_use;
+  }
+  r.cv.notify_all();
+}
+
+int sample_ring_max_in_use(brr_session *s) { return s->ring.max_in_use; }
+
+void sample_ring_close(brr_session *s) {
+  SampleRing &r = s->ring;
+  if (r.depth == 0) return;
+  (void)hipSetDevice(s->device);
+  if (r.cst) (void)hipStreamSynchronize(r.cst);
+  for (int i = 0; i < r.depth; ++i) {
+    if (r.dbuf[i]) (void)hipFree(r.dbuf[i]);
+    if (r.hbuf[i]) (void)hipHostFree(r.hbuf[i]);
+    if (r.ev_snap[i]) (void)hipEventDestroy(r.ev_snap[i]);
+    if (r.ev_host[i]) (void)hipEventDestroy(r.ev_host[i]);
+  }
+  if (r.cst) (void)hipStreamDestroy(r.cst);
+  r.cst = nullptr;
+  r.depth = 0;
+  r.dbuf.clear(); r.hbuf.clear(); r.ev_snap.clear(); r.ev_host.clear(); r.busy.clear();
+}
+
+}  // namespace brr

@@ -211,6 +211,21 @@ class Session:
                 s.update(sigmaF=self.scalar(L.SIGMAF), alpha=self.vector(L.ALPHA))
         return s
 
+    # -- sample output ----------------------------------------------------------
+    def output_open(self, path, header=True, ring_depth=4):
+        """Reference CSV of kept sweeps (asynchronous: device snapshot -> pinned ring -> writer)."""
+        L.check(L.lib().brr_session_output_open(self.h, str(path).encode(), self.model, self.N, self.M,
+                                                self.G, self.F, 1 if header else 0, ring_depth), "output_open")
+
+    def output_sample(self, iteration):
+        L.check(L.lib().brr_session_output_sample(self.h, iteration), "output_sample")
+
+    def output_close(self):
+        """Drains the writer; returns the most rows ever in flight (bounded by ring_depth)."""
+        m = C.c_int32()
+        L.check(L.lib().brr_session_output_close(self.h, C.byref(m)), "output_close")
+        return m.value
+
     # -- instrumentation ----------------------------------------------------------------
     def set_timing(self, on: bool):
         L.check(L.lib().brr_session_set_timing(self.h, 1 if on else 0), "set_timing")

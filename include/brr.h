@@ -203,6 +203,17 @@ int brr_group_init(brr_group *g, int32_t seed);
 int brr_group_sweep(brr_group *g, int32_t n);
 void brr_group_destroy(brr_group *g);
 
+/* sample output for callers that drive sweeps themselves: the one-shots' pipeline
+ * (a device snapshot per kept sweep, an asynchronous copy into a ring of ring_depth pinned host
+ * slots, a writer thread formatting the reference's CSV row; the caller blocks only when the
+ * writer is ring_depth rows behind).  model/N/M/groups/F select the reference's row and header
+ * layout (header = 0: none, as BRV2Grstart).  close drains every queued row; max_rows_in_flight
+ * (may be NULL) reports the most slots ever in use. */
+int brr_session_output_open(brr_session *s, const char *path, int32_t model, int64_t N, int64_t M,
+                            int32_t groups, int64_t F, int32_t header, int32_t ring_depth);
+int brr_session_output_sample(brr_session *s, int32_t iteration);
+int brr_session_output_close(brr_session *s, int32_t *max_rows_in_flight);
+
 /* state read-back (host buffers) */
 enum brr_scalar { BRR_MU = 0, BRR_SIGMAE, BRR_SIGMAG, BRR_SIGMAF, BRR_TAU, BRR_ETA, BRR_C2,
                   BRR_SUMSQ_BETA, BRR_N_SCALARS };

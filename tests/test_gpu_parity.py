@@ -552,3 +552,27 @@ def test_failed_census_exits_cleanly(brr, oracle_mod, require_gpu, monkeypatch):
     resid = Y - s.scalar(L.MU) - X.astype(np.float64) @ s.vector(L.BETA)
     assert _rel(s.vector(L.EPS), resid) < 1e-9
     assert not np.array_equal(s.vector(L.EPS), eps0)
+
+
+@pytest.mark.parametrize("depth", [1, 4])
+def test_session_output_matches_oneshot(brr, oracle_mod, require_gpu, tmp_path, depth, monkeypatch):
+    """The asynchronous sample pipeline (device snapshot -> pinned ring -> writer thread, SURVEY
+    8f2): a session driving its own sweeps with brr_session_output_* writes the one-shot's file
+    byte for byte, at any ring depth (depth 1 = the sampler waits for every row), and never has
+    more rows in flight than the ring holds."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    X, Y, _ = _cohort(O, 150, 200, n_causal=10)
+    p1, p2 = str(tmp_path / "oneshot.csv"), str(tmp_path / "session.csv")
+    monkeypatch.setenv("BRR_SAMPLE_RING", str(depth))
+    brr.BayesRSamplerV2(p1, 5, 12, 2, 1, X, Y, HYP["sigma0"], HYP["v0E"], HYP["s02E"], HYP["v0G"], HYP["s02G"],
+                        CVA, log=lambda m: None)
+    s = brr.Session(L.MODEL_V2, 150, 200, K=4)
+    s.upload_x(X).set_y(Y).set_bayesr(cva=CVA, **HYP).init(5)
+    s.output_open(p2, ring_depth=depth)
+    for it in range(12):
+        s.sweep(1)
+        if it >= 2:
+            s.output_sample(it)
+    assert 1 <= s.output_close() <= depth
+    assert open(p1).read() == open(p2).read()
