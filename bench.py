@@ -129,6 +129,17 @@ def parse():
     ap.add_argument("--shard", default="cols", choices=["cols", "rows"],
                     help="N > 1: column shards with one residual all-reduce per sweep (north_star, SURVEY 8e; "
                          "default) or exact row shards with an all-reduce of each block's dots (SURVEY 8f4)")
+    ap.add_argument("--emit", default=None, metavar="PATH",
+                    help="output-on run (BASELINE.md): write the reference CSV of every --emit-thin'th timed sweep "
+                         "through the asynchronous sample pipeline (SURVEY 8f2), drained inside the timed region")
+    ap.add_argument("--emit-thin", type=int, default=10, help="thinning of the output-on run (vignette: 10)")
+    ap.add_argument("--oneshot", action="store_true",
+                    help="C1 as BASELINE.md states it: the drop-in one-shot brr_BayesRSamplerV2 on host data "
+                         "(N=2,000 x P=10,000, 1,000 iterations, burn-in 500, thinning 10, CSV written), timed "
+                         "end to end, beside the CPU oracle's one-shot on the same data")
+    ap.add_argument("--cpu-iters", type=int, default=100,
+                    help="--oneshot: iterations of the CPU oracle's run (extrapolated to the full run; "
+                         "0 = the full max_iterations)")
     ap.add_argument("--x-storage", default="f32", choices=["f32", "2bit"],
                     help="genotype storage on the device: dense f32 (the BASELINE configs) or 2-bit codes "
                          "+ per-column value tables (SURVEY 8f3; decoded values identical to f32)")
@@ -249,10 +260,86 @@ def spawn_ranks(n: int) -> int:
     return bad[0] if bad else 0
 
 
+def c1_data(N, P, seed):
+    """Host synthetic cohort of the BASELINE spec (numpy: Binomial(2, f), f ~ U(0.05, 0.5), columns
+    standardised with the N-1 sd, min(1000, P/10) causal effects, h2 = 0.5, Y standardised)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    f = rng.uniform(0.05, 0.5, P)
+    G = rng.binomial(2, f, size=(N, P)).astype(np.float64)
+    sd = G.std(axis=0, ddof=1)
+    G = (G - G.mean(axis=0)) / np.where(sd > 0, sd, 1.0)
+    X = np.asfortranarray(G.astype(np.float32).astype(np.float64))
+    nc = max(1, min(1000, P // 10))
+    b = np.zeros(P)
+    b[rng.choice(P, nc, replace=False)] = rng.normal(0, np.sqrt(0.5 / nc), nc)
+    y = X @ b + rng.normal(0, np.sqrt(0.5), N)
+    return X, (y - y.mean()) / y.std(ddof=1)
+
+
+def cpu_oneshot_child(args):
+    """--oneshot CPU leg (one pinned core): the oracle's reference-faithful one-shot."""
+    import numpy as np
+    os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
+    from oracle import oracle as O
+    O.build()
+    X, Y = c1_data(2000, 10000, args.data_seed)
+    it = args.cpu_iters
+    t0 = time.perf_counter()
+    O.run_csv("/tmp/brr_c1_cpu.csv", O.V2, X, Y, it, it // 2, 10, cva=CVA, seed=args.seed, order_mode=0, **HYP)
+    print(json.dumps({"t_s": time.perf_counter() - t0, "iters": it}))
+
+
+def main_oneshot(args):
+    """C1 (BASELINE configs[0]) through the drop-in entry point, end to end."""
+    import numpy as np
+    import bayesrrcpp_amd as B
+    N, P, MAXIT, BURN, THIN = 2000, 10000, 1000, 500, 10
+    X, Y = c1_data(N, P, args.data_seed)
+    out = os.path.join(REPO, "gpurun_out", "c1_oneshot.csv")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    B.BayesRSamplerV2(out, args.seed, 5, 1, 1, X[:, :512].copy(order="F"), Y, HYP["sigma0"], HYP["v0E"],
+                      HYP["s02E"], HYP["v0G"], HYP["s02G"], CVA, log=lambda m: None)  # warm (module load)
+    t0 = time.perf_counter()
+    B.BayesRSamplerV2(out, args.seed, MAXIT, BURN, THIN, X, Y, HYP["sigma0"], HYP["v0E"], HYP["s02E"],
+                      HYP["v0G"], HYP["s02G"], CVA, log=lambda m: None)
+    dt = time.perf_counter() - t0
+    rows = sum(1 for _ in open(out)) - 1
+    cpu = None
+    if not args.no_cpu_baseline:
+        cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--oneshot",
+               "--cpu-iters", str(args.cpu_iters or MAXIT), "--data-seed", str(args.data_seed), "--seed", str(args.seed)]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=3000)
+        if r.returncode == 0:
+            c = json.loads(r.stdout.strip().splitlines()[-1])
+            cpu = {"value": c["iters"] / c["t_s"], "unit": "sweeps/s" + (" (extrapolated from a shorter run)"
+                                                                          if c["iters"] < MAXIT else ""),
+                   "cores": 1, "kind": "port", "host_cpu": host_cpu_model(), "host_nproc": os.cpu_count(),
+                   "sample": f"CPU oracle one-shot (reference-faithful C restatement, 1 pinned core), "
+                             f"{c['iters']} iterations of the same data, CSV written, {c['t_s']:.1f} s"}
+        else:
+            cpu = {"value": None, "sample": "failed: " + r.stderr[-300:]}
+    print(json.dumps({
+        "metric": METRIC, "value": round(MAXIT / dt, 3), "unit": "sweeps/s (end to end: upload, init, 1,000 sweeps, CSV)",
+        "n_gpus": 1, "steps": MAXIT, "warmup": 0, "ms_per_step": round(dt / MAXIT * 1e3, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic host cohort (numpy Binomial(2,f), standardised, f32-representable), f64 arithmetic",
+        "config": {"workload": "C1: brr_BayesRSamplerV2 one-shot N=2,000 x P=10,000, 1,000 iterations, burn-in 500, "
+                               "thinning 10 (BASELINE configs[0], vignettes/BayesRR.Rmd:93-100)",
+                   "wall_s": round(dt, 3), "csv_rows": rows, "csv_bytes": os.path.getsize(out)},
+        "roofline": None, "cpu_baseline": cpu}), flush=True)
+
+
 def main():
     args = parse()
+    if args.cpu_baseline_child and args.oneshot:
+        cpu_oneshot_child(args)
+        return
     if args.cpu_baseline_child:
         cpu_baseline_child(args)
+        return
+    if args.oneshot:
+        main_oneshot(args)
         return
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None:
@@ -348,8 +435,22 @@ def main():
     else:
         s.sweep(args.warmup)
     barrier()
+    emit = None
     t0 = time.perf_counter()
-    s.sweep(args.steps)
+    if args.emit:
+        path = args.emit if world == 1 else f"{args.emit}.rank{rank}"
+        s.output_open(path, header=True, ring_depth=4)
+        rows = 0
+        for k in range(args.steps):
+            s.sweep(1)
+            if k % args.emit_thin == 0:
+                s.output_sample(args.warmup + k)
+                rows += 1
+        inflight = s.output_close()  # every row formatted and written
+        emit = {"path": path, "thinning": args.emit_thin, "rows": rows, "max_rows_in_flight": inflight,
+                "bytes": os.path.getsize(path)}
+    else:
+        s.sweep(args.steps)
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -450,7 +551,8 @@ def main():
                        "x_storage": args.x_storage, "N": N, "P": P, "K": K, "groups": G,
                        "block_size": Bsz, "order": "blocked", "fused_stream_wg": int(s.scalar(104)), "code_cache": int(s.scalar(105)), "pipeline_lag": int(s.scalar(106)),
                        "parallelism": f"row-shard x{world} (exact)" if rows else f"column-shard x{world}",
-                       "setup_s": round(t_setup, 2), "diag": diag},
+                       "setup_s": round(t_setup, 2), "diag": diag,
+                       **({"output": emit} if emit else {})},
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -16,6 +16,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace -o
 f=$(find gpurun_out/${TAG}_trace -name "*kernel_stats.csv" | head -1)
 cp "$f" gpurun_out/${TAG}_kernel_stats.csv
 cut -c1-200 gpurun_out/${TAG}_kernel_stats.csv | head -8
+python3 scripts/steady_stats.py gpurun_out/${TAG}_trace 10 gpurun_out/${TAG}_ksweep || exit 1
 tail -1 gpurun_out/${TAG}_trace.log | cut -c1-400
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex 'k_sweep' -d gpurun_out/${TAG}_pmc_$c -o pmc \
