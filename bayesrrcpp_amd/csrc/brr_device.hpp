@@ -4,10 +4,14 @@
 //   X        f32, column-major, ld = roundup(N, 256) rows (1-KiB aligned columns, zero rows
 //            beyond N, so a streaming row tile never leaves the allocation); the only
 //            large array: streamed once per sweep by k_stream.
-//   Xc+xlut  alternative genotype storage: 2-bit codes, column-major, ld/4 bytes
-//            per column (PLINK .bed packing), and a 4-entry f32 value table per column.  The
-//            decoded values are the f32 values the X storage would hold, so every kernel
-//            computes on bit-identical inputs; a sweep reads N P / 4 bytes instead of 4 N P.
+//   Xc+xlut  alternative genotype storage: 2-bit codes (a byte = 4 consecutive rows of
+//            one column, PLINK .bed packing) in tiles, and a 4-entry f32 value table per column.
+//            Tile order: column block b (B columns), group of 16 columns, row quad g (nq = ld/4 =
+//            ldc quads), 16 bytes = the group's 16 columns at that quad: byte of (b B + i, g) at
+//            ((b B/16 + i/16) nq + g) 16 + i%16 (code_off).  A streaming lane reads 16 columns x 4
+//            rows with one 16-byte load and a wave 1 KiB contiguous.  The decoded values are the
+//            f32 values the X storage would hold, so every kernel computes on bit-identical
+//            inputs; a sweep reads N P / 4 bytes instead of 4 N P.
 //   eps,eps2 f64 [ld] residual (Y - mu - X beta), double-buffered across k_stream launches.
 //   beta,xsq f64 [M]; comp int32 [M]; sel uint8 [M] (marker selected a component this sweep)
 //   gram     f64 [nb][B][B] block Gram matrices X_b^T X_b of the fixed column blocks.
@@ -92,13 +96,14 @@ struct Dev {
   int64_t Ntot, row_offset;  // row shards: cohort rows and this shard's first row (else N, 0)
   int K, G, F, B, nb, model, R, RG, NG, MRG;
   int gtarget;      // reduction groups k_solve(s) waits for (per-block: NG * NC; persistent: NG)
+  int slab_storage; // the partial dots are indexed by in-block storage index, not visit position
+                    // (fused sweep on 2-bit code tiles)
   uint64_t seed;
   Hyper hyp;
   const float *X;      // f32 storage (x_storage BRR_X_F32), else nullptr
   const uint8_t *Xc;   // 2-bit genotype codes (BRR_X_2BIT), else nullptr: column j at Xc + j ldc,
                        // row i in bits 2(i&3)..2(i&3)+1 of byte i>>2 (PLINK .bed packing)
   const float *xlut;   // [M][4] value of each code of column j (padding rows decode to 0)
-  float4 *xlut_ord;    // [nb B] value tables in this sweep's visit order (k_lut_order)
   int64_t ldc;         // bytes per code column = ld / 4
   const double *Y, *fixed, *cva;
   const int *gAssign;

@@ -91,14 +91,20 @@ __device__ __forceinline__ float4 x_decode4(uint32_t b, float4 l) {
 __device__ __forceinline__ float4 x_lut(const Dev &d, int64_t col) {
   return *reinterpret_cast<const float4 *>(d.xlut + 4 * col);
 }
+// 2-bit code tiles (brr_device.hpp): byte of (column col, row quad g) -- column col = b B + i of
+// block b, group i / 16 of 16 columns, quad g: ((b B/16 + i/16) nq + g) 16 + i % 16, nq = ldc
+__host__ __device__ __forceinline__ int64_t code_off(int64_t col, int64_t g, int B, int64_t nq) {
+  const int64_t b = col / B, i = col - b * B;
+  return ((b * (B >> 4) + (i >> 4)) * nq + g) * 16 + (i & 15);
+}
 // one value (scattered reads: change lists, synthetic Y)
 __device__ __forceinline__ float x_at(const Dev &d, int64_t col, int64_t row) {
-  if (d.Xc) return x_sel(x_lut(d, col), (uint32_t)d.Xc[col * d.ldc + (row >> 2)] >> (2 * (row & 3)));
+  if (d.Xc) return x_sel(x_lut(d, col), (uint32_t)d.Xc[code_off(col, row >> 2, d.B, d.ldc)] >> (2 * (row & 3)));
   return d.X[col * d.ld + row];
 }
 // four consecutive rows row4 .. row4+3 (row4 a multiple of 4)
 __device__ __forceinline__ float4 x_at4(const Dev &d, int64_t col, int64_t row4) {
-  if (d.Xc) return x_decode4(d.Xc[col * d.ldc + (row4 >> 2)], x_lut(d, col));
+  if (d.Xc) return x_decode4(d.Xc[code_off(col, row4 >> 2, d.B, d.ldc)], x_lut(d, col));
   return *reinterpret_cast<const float4 *>(d.X + col * d.ld + row4);
 }
 
@@ -222,7 +228,8 @@ __device__ __forceinline__ int genotype(uint64_t ds, int64_t i, int64_t j, uint3
 // Row shards: the column statistics run over all Ntot rows of the cohort (the
 // genotypes are counter-based, so every shard draws them), only rows [row0, row0 + N) are stored.
 __global__ __launch_bounds__(256) void k_synth_x(float *X, uint8_t *Xc, float *xlut, int64_t ld, int64_t ldc,
-                                                 int64_t N, int64_t col0, uint64_t ds, int64_t Ntot, int64_t row0) {
+                                                 int64_t N, int64_t col0, uint64_t ds, int64_t Ntot, int64_t row0,
+                                                 int B) {
 #pragma clang fp contract(off)
   __shared__ double red[8];
   __shared__ int s_att;
@@ -257,7 +264,6 @@ __global__ __launch_bounds__(256) void k_synth_x(float *X, uint8_t *Xc, float *x
       const int g = threadIdx.x;
       xlut[4 * jl + g] = (mono || g == 3) ? 0.f : (float)(((double)g - mean) / sd);
     }
-    uint8_t *xc = Xc + jl * ldc;
     for (int64_t b = threadIdx.x; b < ldc; b += 256) {
       uint32_t byte = 0;
 #pragma unroll
@@ -266,7 +272,7 @@ __global__ __launch_bounds__(256) void k_synth_x(float *X, uint8_t *Xc, float *x
         const uint32_t c = (mono || i >= N) ? 3u : (uint32_t)genotype(ds, row0 + i, j, att, t0, t1);
         byte |= c << (2 * k);
       }
-      xc[b] = (uint8_t)byte;
+      Xc[code_off(jl, b, B, ldc)] = (uint8_t)byte;
     }
     return;
   }
@@ -279,6 +285,14 @@ __global__ __launch_bounds__(256) void k_synth_x(float *X, uint8_t *Xc, float *x
     if (i < N) v = (float)(((double)genotype(ds, row0 + i, j, att, t0, t1) - mean) / sd);
     x[i] = v;
   }
+}
+
+// 2-bit upload: a chunk of nc column-major code columns (ldc bytes each) into the code tiles
+__global__ __launch_bounds__(256) void k_codes_tile(const uint8_t *src, uint8_t *Xc, int64_t c0, int64_t nc,
+                                                    int64_t ldc, int B) {
+  const int64_t jj = blockIdx.y;
+  for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < ldc; g += (int64_t)gridDim.x * 256)
+    Xc[code_off(c0 + jj, g, B, ldc)] = src[jj * ldc + g];
 }
 
 // y_i = sum_{causal j} x_ij beta_j  (causal list from the host)
@@ -343,8 +357,8 @@ __global__ __launch_bounds__(256) void k_gram(Dev d, const int *member, const in
     for (int q = 0; q < 16; q += 4) {
       float4 va, vb;
       if (d.Xc) {  // 2-bit codes: the same f32 values, decoded
-        va = ca >= 0 ? x_decode4(d.Xc[ca * d.ldc + ((r0 + lr + q) >> 2)], la) : z4;
-        vb = cb >= 0 ? x_decode4(d.Xc[cb * d.ldc + ((r0 + lr + q) >> 2)], lb) : z4;
+        va = ca >= 0 ? x_decode4(d.Xc[code_off(ca, (r0 + lr + q) >> 2, d.B, d.ldc)], la) : z4;
+        vb = cb >= 0 ? x_decode4(d.Xc[code_off(cb, (r0 + lr + q) >> 2, d.B, d.ldc)], lb) : z4;
       } else {
         va = pa ? *reinterpret_cast<const float4 *>(pa + r0 + lr + q) : z4;
         vb = pb ? *reinterpret_cast<const float4 *>(pb + r0 + lr + q) : z4;
@@ -505,13 +519,6 @@ __global__ void k_perm_within(Dev d, uint32_t it, int identity) {
     d.gidx[(int64_t)s * d.B + i] = i < size ? w[i] : 0;
   }
   if (threadIdx.x == 0) { d.bsz[s] = size; d.gblk[s] = b; }
-}
-
-// 2-bit storage: the value tables in visit order, so a streaming workgroup stages a block's
-// tables with one independent 16-B load per position.
-__global__ __launch_bounds__(256) void k_lut_order(Dev d) {
-  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (q < d.nbB) d.xlut_ord[q] = x_lut(d, d.member[q]);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1654,10 +1661,13 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     bool likely = false;
     if (pos < bs) {
       double dsum = 0.0;
+      // the dots are by visit position, or by in-block (storage) index when the 2-bit streamers
+      // read the block in storage order
+      const int sidx = d.slab_storage ? Lgi[pos] : pos;
       for (int g0 = 0; g0 < d.NG; g0 += 16) {
         double v[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = g0 + u < d.NG ? ld_sc1(slab2 + (int64_t)(g0 + u) * B + pos) : 0.0;
+        for (int u = 0; u < 16; ++u) v[u] = g0 + u < d.NG ? ld_sc1(slab2 + (int64_t)(g0 + u) * B + sidx) : 0.0;
 #pragma unroll
         for (int u = 0; u < 16; ++u) dsum += v[u];
       }
@@ -2091,7 +2101,7 @@ constexpr int SWEEP_NW = SWEEP_NT / 64;
 #define STREAM_P 1    // items in flight ahead of the one being consumed (2+ spills at CW = 16)
 #endif
 #ifndef STREAM_P2
-#define STREAM_P2 3   // the same for 2-bit codes (a byte per column and lane; vmcnt <= 63 caps P CW)
+#define STREAM_P2 6   // the same for 2-bit code tiles (one 16-byte load per item and lane)
 #endif
 // streaming workgroups (slab rows) per level-2 reduction group: 64 -> 4 reducer workgroups at C2
 // (16 / 32 / 64 measured 27.1 / 27.6 / 28.1 sweeps/s: fewer reducers, fewer slab2 rows for the
@@ -2114,8 +2124,9 @@ constexpr int FUSED_GROUP = FUSED_GROUP_N;
 // msrc != nullptr: also copy the B member indices at msrc to mdst (LDS); loaded before the first
 // barrier, stored after the last (the buffer's previous block is then no longer read by any wave).
 // ccode != nullptr (2-bit storage): the code bytes of the block being applied are in LDS
-// (stream_role's code cache, ccode[pos * npass * 64 + row / 4]); s_ppos receives the positions.
-// 2-bit storage: lsrc / ldst stage the next block's value tables the same way; lutb = the value
+// (stream_role's code cache, tiles [group][row quad][16]); s_ppos receives the in-block indices.
+// 2-bit storage: lsrc / ldst stage the next block's value tables (storage order, lcnt valid
+// entries) the same way; lutb = the value
 // tables of the block being applied (LDS, by visit position).
 template <int XF>
 __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0, int64_t r1, int npass,
@@ -2123,7 +2134,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
                                               int *s_np, double *s_part, const int *msrc = nullptr,
                                               int *mdst = nullptr, const uint8_t *ccode = nullptr,
                                               int *s_ppos = nullptr, const float4 *lsrc = nullptr,
-                                              float4 *ldst = nullptr, const float4 *lutb = nullptr) {
+                                              float4 *ldst = nullptr, const float4 *lutb = nullptr, int lcnt = 0) {
 #pragma clang fp contract(off)
   constexpr int AB = 4;  // columns per batch (two batches in flight: 8 KiB per wave, 32 VGPRs, as many as the
                          // streaming ring leaves without spills)
@@ -2132,7 +2143,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
   const bool mcopy = msrc != nullptr && t < d.B;
   const int mval = mcopy ? msrc[t] : 0;
   const bool lcopy = XF && lsrc != nullptr && t < d.B;
-  const float4 lval = lcopy ? lsrc[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 lval = (lcopy && t < lcnt) ? lsrc[t] : make_float4(0.f, 0.f, 0.f, 0.f);
   double *s_pd = s_pbo;  // b_old - b_new per list entry
   (void)s_pbn;
   if (t < 64) {
@@ -2145,7 +2156,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
       // hit instead of column 0 from HBM, and no branch in the batched loads
       const int es = e < nr ? e : max(nr - 1, 0);
       s_pidx[e] = ld_sc1_int(pidx + es);
-      if (XF) s_ppos[e] = ld_sc1_int(d.pend_pos + slot * d.pend_stride + es);
+      if (XF) s_ppos[e] = ld_sc1_int(d.pend_gi + slot * d.pend_stride + es);  // in-block (storage) index
       s_pd[e] = ld_sc1(pbo + e) - ld_sc1(pbn + e);
     }
     if (lane == 0) s_np[0] = np;
@@ -2164,10 +2175,12 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
       const int64_t src = ok ? r0 + off : r0;  // lanes past the rows re-read row r0 (not stored)
       auto xload = [&](int e) __attribute__((always_inline)) -> float4 {
         if constexpr (XF) {
-          const int pos = s_ppos[e];
-          const uint32_t byte = ccode ? (uint32_t)ccode[pos * (npass * 64) + (off >> 2)]
-                                      : (uint32_t)d.Xc[(int64_t)s_pidx[e] * d.ldc + (src >> 2)];
-          return x_decode4(byte, lutb[pos]);
+          // code byte of (column, this lane's row quad): from the LDS code cache (tiles of this
+          // workgroup's rows, stream_role) or the HBM code tiles
+          const int gi = s_ppos[e];
+          const uint32_t byte = ccode ? (uint32_t)ccode[((gi >> 4) * (npass * 64) + (off >> 2)) * 16 + (gi & 15)]
+                                      : (uint32_t)d.Xc[code_off(s_pidx[e], src >> 2, d.B, d.ldc)];
+          return x_decode4(byte, lutb[gi]);
         } else {
           return ldg4(d.X + (int64_t)s_pidx[e] * d.ld + src);
         }
@@ -2239,10 +2252,13 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
   __syncthreads();
 }
 
-// XF = 1: 2-bit genotype codes.  The ring then holds one code byte (4 rows) per column and lane,
-// and the value tables of the block being consumed are staged in LDS (s_lut, B entries) at each
-// block boundary, after the previous block's last item and before the barrier that precedes the
-// first item of the block.
+// XF = 1: 2-bit genotype codes in tiles (brr_device.hpp).  A block is streamed in STORAGE order:
+// item (chunk c of wave w, pass p) = the block's 16-column group w CPW / 16 + c and this lane's row
+// quad, ONE 16-byte load per lane (1 KiB per wave instruction, 16 columns x 256 rows), so the
+// partial dot of in-block column i lands in slab column i (the solver reads it by Gram index,
+// Dev::slab_storage).  The value tables of the block being consumed are staged in LDS in storage
+// order (s_lut, B entries) at each block boundary, after the previous block's last item and
+// before the barrier that precedes the first item of the block.
 template <int CW, int P, int XF>
 __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int npass, double *eps_l, int *s_pidx,
                                             double *s_pbo, double *s_pbn, int *s_np, float4 *s_lut, int *s_mem,
@@ -2262,7 +2278,9 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   auto lut_of = [&](int s) __attribute__((always_inline)) { return s_lut + (int64_t)(s % NLB) * B; };
   auto stage_lut = [&](int s) __attribute__((always_inline)) {
     if constexpr (XF) {
-      for (int i = t; i < B; i += SWEEP_NT) lut_of(s)[i] = d.xlut_ord[(int64_t)s * B + i];
+      const int gb = d.gblk[s], bs = d.bsz[s];
+      const float4 *src = reinterpret_cast<const float4 *>(d.xlut) + (int64_t)gb * B;
+      for (int i = t; i < B; i += SWEEP_NT) lut_of(s)[i] = i < bs ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
   for (int i = t; i < npass * SROWS; i += SWEEP_NT) eps_l[i] = r0 + i < r1 ? d.eps[r0 + i] : 0.0;
@@ -2275,8 +2293,9 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   __syncthreads();
   const int CPW = B / SWEEP_NW;  // columns per wave
   const int NCH = CPW / CW;      // chunks per wave and block
-  // 2-bit storage with room in LDS: the code bytes of this workgroup's rows of the last three
-  // blocks (buffer s % 3), so the change list of block s - 2 is applied from LDS, not HBM
+  // 2-bit storage with room in LDS: the code tiles of this workgroup's rows of the last LAG + 2
+  // blocks (buffer s % NCC; [group][row quad][16 columns]), so the change list of block s-1-LAG is
+  // applied from LDS, not HBM
   auto cache_of = [&](int s) __attribute__((always_inline)) -> const uint8_t * {
     return (XF && s_codes) ? s_codes + (int64_t)(s % NCC) * B * (npass * 64) : nullptr;
   };
@@ -2287,16 +2306,19 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   // residual rows are 0, so they add exactly 0); rows in [N, ld) are zero padding of X.  The
   // loads stay unconditional: a divergent branch here would turn the wave-uniform member
   // loads into vector loads whose wait drains the prefetch ring.
-  using Raw = typename std::conditional<XF != 0, uint32_t, float4>::type;
-  auto issue = [&](int it, Raw (&x)[CW]) {
+  // f32: one float4 (4 rows) per column and lane; 2-bit: one 16-byte code group (16 columns x 4
+  // rows) per lane in x[0]
+  using Raw = typename std::conditional<XF != 0, uint4, float4>::type;
+  constexpr int NR = XF ? 1 : CW;
+  auto issue = [&](int it, Raw (&x)[NR]) {
     const int s = it / items, rem = it - s * items;
     const int c = rem / npass, p = rem - c * npass;
     const int64_t off = r0 + p * SROWS + 4 * lane < r1 ? r0 + p * SROWS + 4 * lane : r0;
     if constexpr (XF) {
-      const int *mem = d.member + (int64_t)s * B + w * CPW + c * CW;  // wave-uniform: scalar loads
-      const uint8_t *base = d.Xc + (off >> 2);
-#pragma unroll
-      for (int j = 0; j < CW; ++j) x[j] = base[(int64_t)mem[j] * d.ldc];
+      static_assert(CW == 16, "a 2-bit item is one 16-column group");
+      const int64_t gb = d.gblk[s];  // wave-uniform
+      const int64_t grp = gb * (B >> 4) + ((w * CPW + c * CW) >> 4);
+      x[0] = *reinterpret_cast<const uint4 *>(d.Xc + (grp * d.ldc + (off >> 2)) * 16);
     } else {
       const float *base = d.X + off;
       // (scalar loads of the member indices instead: -6 % at C2, a K$ miss per item)
@@ -2312,7 +2334,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     }
   };
   // register ring of P + 1 items: item it + P is issued before item it is consumed
-  Raw xq[P + 1][CW];
+  Raw xq[P + 1][NR];
   double v[CW];
 #pragma unroll
   for (int j = 0; j < CW; ++j) v[j] = 0.0;
@@ -2352,8 +2374,9 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       }
       apply_pending<XF>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, s_part,
                         (!XF && s + 1 < nb) ? d.member + (int64_t)(s + 1) * B : nullptr, s_mem + ((s + 1) & 1) * B,
-                        cache_of(a), s_mem, (XF && s + 1 < nb) ? d.xlut_ord + (int64_t)(s + 1) * B : nullptr,
-                        lut_of(s + 1), lut_of(a));
+                        cache_of(a), s_mem,
+                        (XF && s + 1 < nb) ? reinterpret_cast<const float4 *>(d.xlut) + (int64_t)d.gblk[s + 1] * B : nullptr,
+                        lut_of(s + 1), lut_of(a), (XF && s + 1 < nb) ? d.bsz[s + 1] : 0);
       if (prof && t == 0) {
         tr_last(d, s, TR_APPLY_LAST);
         if (s == nb / 2) d.trace[(int64_t)nb * 16 + 1024 + g] = wall_clock64();  // per-workgroup probe
@@ -2367,13 +2390,18 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     if (!blk_end && it + P < total) issue(it + P, xq[P]);
     const double *e = eps_l + p * SROWS + 4 * lane;
     const double e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
+    if constexpr (XF) {
+      // code cache: block s's tile of group w CPW / 16 + c at this lane's row quad p 64 + lane
+      if (s_codes)
+        reinterpret_cast<uint4 *>(s_codes)[((s % NCC) * (B >> 4) + ((w * CPW + c * CW) >> 4)) * (npass * 64) + p * 64 +
+                                           lane] = xq[0][0];
+    }
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
       float4 xv;
       if constexpr (XF) {
-        xv = x_decode4(xq[0][j], lut_of(s)[w * CPW + c * CW + j]);
-        // code cache: block s's bytes at position w CPW + c CW + j, row byte p 64 + lane
-        if (s_codes) s_codes[((s % NCC) * B + w * CPW + c * CW + j) * (npass * 64) + p * 64 + lane] = (uint8_t)xq[0][j];
+        const uint32_t word = j < 4 ? xq[0][0].x : (j < 8 ? xq[0][0].y : (j < 12 ? xq[0][0].z : xq[0][0].w));
+        xv = x_decode4((word >> (8 * (j & 3))) & 0xFFu, lut_of(s)[w * CPW + c * CW + j]);
       } else {
         xv = xq[0][j];
       }
@@ -2382,7 +2410,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
 #pragma unroll
     for (int q = 0; q < P; ++q)
 #pragma unroll
-      for (int j = 0; j < CW; ++j) xq[q][j] = xq[q + 1][j];
+      for (int j = 0; j < NR; ++j) xq[q][j] = xq[q + 1][j];
     if (p == npass - 1) {
       // chunk done over this workgroup's rows: wave-reduce its CW columns
       double r;
@@ -2405,7 +2433,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       // issue order) without draining the prefetch.
       asm volatile("" ::: "memory");
       if (it + P < total) issue(it + P, xq[P - 1]);
-      if (it + P < total) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P * CW) : "memory");
+      if (it + P < total) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P * NR) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // then one arrival on the group counter for the reducer workgroup (one per workgroup:
       // per-wave arrivals measured 1.6x slower, contention on the group counters)
@@ -2719,12 +2747,21 @@ static inline unsigned cdiv64(int64_t a, int64_t b) { return (unsigned)((a + b -
 hipError_t launch_synth_x(const Dev &d, uint64_t ds, hipStream_t st) {
   hipLaunchKernelGGL(k_synth_x, dim3((unsigned)d.M), dim3(256), 0, st, const_cast<float *>(d.X),
                      const_cast<uint8_t *>(d.Xc), const_cast<float *>(d.xlut), d.ld, d.ldc, d.N, d.col_offset, ds,
-                     d.Ntot, d.row_offset);
+                     d.Ntot, d.row_offset, d.B);
   return hipGetLastError();
 }
 
 hipError_t launch_synth_y(const Dev &d, const int *cidx, const double *cb, int nc, double *y, hipStream_t st) {
   hipLaunchKernelGGL(k_synth_y, dim3(cdiv64(d.N, 256)), dim3(256), 0, st, d, cidx, cb, nc, y);
+  return hipGetLastError();
+}
+
+hipError_t launch_codes_tile(const uint8_t *src, uint8_t *Xc, int64_t c0, int64_t nc, int64_t ldc, int B,
+                             hipStream_t st) {
+  for (int64_t j0 = 0; j0 < nc; j0 += 65535) {
+    const dim3 grid(cdiv64(ldc, 256) > 64 ? 64 : cdiv64(ldc, 256), (unsigned)std::min<int64_t>(65535, nc - j0));
+    hipLaunchKernelGGL(k_codes_tile, grid, dim3(256), 0, st, src + j0 * ldc, Xc, c0 + j0, grid.y, ldc, B);
+  }
   return hipGetLastError();
 }
 
@@ -2775,11 +2812,6 @@ hipError_t launch_sweep_start(const Dev &d, uint32_t it, hipStream_t st) {
 hipError_t launch_perm(const Dev &d, uint32_t it, int shard, bool identity, hipStream_t st) {
   hipLaunchKernelGGL(k_perm_blockorder, dim3(1), dim3(256), 0, st, d, it, shard, identity ? 1 : 0);
   hipLaunchKernelGGL(k_perm_within, dim3((unsigned)d.nb), dim3(64), 0, st, d, it, identity ? 1 : 0);
-  return hipGetLastError();
-}
-
-hipError_t launch_lut_order(const Dev &d, hipStream_t st) {
-  hipLaunchKernelGGL(k_lut_order, dim3(cdiv64(d.nbB, 256)), dim3(256), 0, st, d);
   return hipGetLastError();
 }
 

@@ -16,7 +16,8 @@ hipError_t launch_synth_x(const Dev &d, uint64_t ds, hipStream_t st);
 hipError_t launch_synth_y(const Dev &d, const int *cidx, const double *cb, int nc, double *y, hipStream_t st);
 hipError_t launch_cast_x(const void *src, bool is_f64, int64_t lds, float *dst, int64_t ldd,
                          int64_t N, int64_t M, hipStream_t st);
-hipError_t launch_lut_order(const Dev &d, hipStream_t st);
+hipError_t launch_codes_tile(const uint8_t *src, uint8_t *Xc, int64_t c0, int64_t nc, int64_t ldc, int B,
+                             hipStream_t st);
 hipError_t launch_gram(const Dev &d, int shift, double *G, double *GT, hipStream_t st);
 hipError_t launch_xsq(const Dev &d, hipStream_t st);
 hipError_t launch_rows(const Dev &d, int flags, const double *deps_in, hipStream_t st,

@@ -302,7 +302,6 @@ int do_sweep_local(brr_session *s) {
   } else {
     HIPCHK(launch_perm(d, it, s->shard, true, s->st));
   }
-  if (d.Xc) HIPCHK(launch_lut_order(d, s->st));
   if (s->model == MODEL_GROUPS && s->F > 0)
     HIPCHK(launch_fixed(d, it, s->order_mode == BRR_ORDER_BLOCKED, s->st));
   if (sharded)
@@ -326,6 +325,7 @@ int do_sweep_local(brr_session *s) {
     Dev dp = d;
     dp.NG = s->fused.ngroups;
     dp.gtarget = s->fused.ngroups;
+    dp.slab_storage = d.Xc != nullptr;  // 2-bit streamers read blocks in storage order
     if (s->timing) {
       const size_t i0 = s->ev_used;
       hipEvent_t e0 = s->ev(), e1 = s->ev();
@@ -591,11 +591,6 @@ int coll_sweep_rows(Coll &c) {
     return rc;
   if (s0->order_mode == BRR_ORDER_REFERENCE)
     if (int rc = coll_grams(c)) return rc;
-  if (int rc = coll_each(c, [](brr_session *s) -> int {
-        if (s->d.Xc) HIPCHK(launch_lut_order(s->d, s->st));
-        return 0;
-      }))
-    return rc;
   if (s0->model == MODEL_GROUPS && s0->F > 0) {
     const bool dev_perm = s0->order_mode == BRR_ORDER_BLOCKED;
     for (int cf = 0; cf < s0->F; ++cf) {
@@ -805,9 +800,8 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   s->x2bit = opt.x_storage == BRR_X_2BIT;
   d.ldc = d.ld / 4;
   if (s->x2bit) {
-    rc |= s->alloc(const_cast<uint8_t **>(&d.Xc), d.ldc * M);
+    rc |= s->alloc(const_cast<uint8_t **>(&d.Xc), d.ldc * s->nb * B);  // whole tiles of the last block
     rc |= s->alloc(const_cast<float **>(&d.xlut), 4 * M);
-    rc |= s->alloc(reinterpret_cast<float **>(&d.xlut_ord), 4 * (int64_t)s->nb * B);
   } else {
     rc |= s->alloc(const_cast<float **>(&d.X), d.ld * M);
   }
@@ -879,7 +873,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
             hipMemsetAsync(d.mcnt, 0, sizeof(int), s->st) == hipSuccess &&
             hipMemsetAsync(d.sc, 0, sizeof(Scal), s->st) == hipSuccess &&
             hipMemsetAsync(d.stats, 0, sizeof(double) * s->NS, s->st) == hipSuccess &&
-            (s->x2bit ? hipMemsetAsync(const_cast<uint8_t *>(d.Xc), 0xFF, (size_t)d.ldc * M, s->st) == hipSuccess &&
+            (s->x2bit ? hipMemsetAsync(const_cast<uint8_t *>(d.Xc), 0xFF, (size_t)d.ldc * s->nb * B, s->st) == hipSuccess &&
                             hipMemsetAsync(const_cast<float *>(d.xlut), 0, sizeof(float) * 4 * M, s->st) == hipSuccess
                       : hipMemsetAsync(const_cast<float *>(d.X), 0, sizeof(float) * d.ld * M, s->st) == hipSuccess) &&
             hipMemsetAsync(d.alpha, 0, sizeof(double) * std::max<int64_t>(F, 1), s->st) == hipSuccess &&
@@ -1018,6 +1012,9 @@ static int upload_x_any(brr_session *s, const void *X, bool f64, int64_t ldx) {
     const int64_t chunk_cols = std::max<int64_t>(1, std::min<int64_t>(s->M, (int64_t)(256ll << 20) / ldc));
     std::vector<uint8_t> codes((size_t)(ldc * chunk_cols));
     std::vector<float> lut((size_t)(4 * chunk_cols));
+    uint8_t *stage = nullptr;  // column-major chunk on the device, scattered into the code tiles
+    HIPCHK(hipMalloc(&stage, (size_t)(ldc * chunk_cols)));
+    struct Free { uint8_t *p; ~Free() { (void)hipFree(p); } } free_stage{stage};
     for (int64_t c0 = 0; c0 < s->M; c0 += chunk_cols) {
       const int64_t nc = std::min<int64_t>(chunk_cols, s->M - c0);
       const int64_t bad = encode_2bit(X, f64, ldx, s->N, ldc, c0, nc, codes.data(), lut.data());
@@ -1026,8 +1023,9 @@ static int upload_x_any(brr_session *s, const void *X, bool f64, int64_t ldx) {
                   "genotype-coded columns (x_storage = BRR_X_F32 stores any matrix)", (long long)bad);
         return -1;
       }
-      HIPCHK(hipMemcpy(const_cast<uint8_t *>(s->d.Xc) + ldc * c0, codes.data(), (size_t)(ldc * nc),
-                       hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(stage, codes.data(), (size_t)(ldc * nc), hipMemcpyHostToDevice));
+      HIPCHK(launch_codes_tile(stage, const_cast<uint8_t *>(s->d.Xc), c0, nc, ldc, s->B, s->st));
+      HIPCHK(hipStreamSynchronize(s->st));
       HIPCHK(hipMemcpy(const_cast<float *>(s->d.xlut) + 4 * c0, lut.data(), sizeof(float) * 4 * nc,
                        hipMemcpyHostToDevice));
     }
@@ -1075,8 +1073,14 @@ int brr_session_upload_bed(brr_session *s, const uint8_t *bed, int64_t bytes_per
   const int64_t chunk_cols = std::max<int64_t>(1, std::min<int64_t>(s->M, (int64_t)(256ll << 20) / ldc));
   std::vector<uint8_t> codes;
   std::vector<float> lut((size_t)(4 * chunk_cols)), xf;
-  if (s->x2bit) codes.resize((size_t)(ldc * chunk_cols));
-  else xf.resize((size_t)(s->d.ld * chunk_cols));
+  uint8_t *stage = nullptr;  // 2-bit: column-major chunk on the device, scattered into the code tiles
+  if (s->x2bit) {
+    codes.resize((size_t)(ldc * chunk_cols));
+    HIPCHK(hipMalloc(&stage, (size_t)(ldc * chunk_cols)));
+  } else {
+    xf.resize((size_t)(s->d.ld * chunk_cols));
+  }
+  struct Free { uint8_t *p; ~Free() { if (p) (void)hipFree(p); } } free_stage{stage};
   static const double gval[4] = {2.0, 0.0 /* missing */, 1.0, 0.0};
   for (int64_t c0 = 0; c0 < s->M; c0 += chunk_cols) {
     const int64_t nc = std::min<int64_t>(chunk_cols, s->M - c0);
@@ -1104,8 +1108,9 @@ int brr_session_upload_bed(brr_session *s, const uint8_t *bed, int64_t bytes_per
       }
     }
     if (s->x2bit) {
-      HIPCHK(hipMemcpy(const_cast<uint8_t *>(s->d.Xc) + ldc * c0, codes.data(), (size_t)(ldc * nc),
-                       hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(stage, codes.data(), (size_t)(ldc * nc), hipMemcpyHostToDevice));
+      HIPCHK(launch_codes_tile(stage, const_cast<uint8_t *>(s->d.Xc), c0, nc, ldc, s->B, s->st));
+      HIPCHK(hipStreamSynchronize(s->st));
       HIPCHK(hipMemcpy(const_cast<float *>(s->d.xlut) + 4 * c0, lut.data(), sizeof(float) * 4 * nc,
                        hipMemcpyHostToDevice));
     } else {
@@ -1460,13 +1465,13 @@ int64_t brr_session_get_vector(brr_session *s, int32_t which, double *out) {
   if (which == 200) {
     std::vector<float> x((size_t)(s->d.ld * s->M));
     if (s->x2bit) {
-      std::vector<uint8_t> c((size_t)(s->d.ldc * s->M));
+      std::vector<uint8_t> c((size_t)(s->d.ldc * s->nb * s->B));
       std::vector<float> l((size_t)(4 * s->M));
       if (int rc = d2h(s, c.data(), s->d.Xc, (int64_t)c.size())) return rc;
       if (int rc = d2h(s, l.data(), s->d.xlut, (int64_t)l.size())) return rc;
       for (int64_t j = 0; j < s->M; ++j)
         for (int64_t i = 0; i < s->d.ld; ++i)
-          x[(size_t)(j * s->d.ld + i)] = l[(size_t)(4 * j + ((c[(size_t)(j * s->d.ldc + (i >> 2))] >> (2 * (i & 3))) & 3))];
+          x[(size_t)(j * s->d.ld + i)] = l[(size_t)(4 * j + ((c[(size_t)((((j / s->B) * (s->B >> 4) + ((j % s->B) >> 4)) * s->d.ldc + (i >> 2)) * 16 + (j % s->B & 15))] >> (2 * (i & 3))) & 3))];
     } else if (int rc = d2h(s, x.data(), s->d.X, (int64_t)x.size())) {
       return rc;
     }
