@@ -734,7 +734,10 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   // keeps most markers in non-zero components (C3: 23 % change per sweep), so their serial chain
   // dominates and B = 128 keeps the whole Gram block in LDS (C3: 9.3 / 6.2 / 4.5 sweeps/s at
   // B = 128 / 256 / 512)
-  int B = opt.block_size > 0 ? opt.block_size : ((model == MODEL_HORSESHOE || model == MODEL_GROUPS) ? 128 : 512);
+  // (small cohorts: the chain, not the stream, dominates every sampler -- C1, N = 2,000: 147 against
+  // 90 sweeps/s at B = 128 / 512 -- so B = 128 below N = 32,768)
+  int B = opt.block_size > 0 ? opt.block_size
+                             : ((model == MODEL_HORSESHOE || model == MODEL_GROUPS || N < 32768) ? 128 : 512);
   if (B % 64 != 0 || B > BMAX) { set_error("block_size=%d must be a multiple of 64 and <= %d", B, BMAX); return nullptr; }
   if (opt.shard_count < 1) opt.shard_count = 1;
   if (opt.shard_count > 1 && (col_offset % B) != 0) {

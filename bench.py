@@ -116,6 +116,9 @@ def parse():
     ap.add_argument("--P", type=int, default=None)
     ap.add_argument("--block-size", type=int, default=0,
                     help="marker block B; 0 = the library's automatic choice (512 V2, 128 Groups and Horseshoe)")
+    ap.add_argument("--order", default="blocked", choices=["blocked", "reference"],
+                    help="visit order: BLOCKED (fast path) or the reference's own std::random_shuffle order "
+                         "(Gram blocks recomputed every sweep)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--data-seed", type=int, default=20261015)
     ap.add_argument("--profile-solve", action="store_true", help="k_solve phase timers (diag)")
@@ -365,18 +368,19 @@ def main():
     N = args.N or cfg["N"]
     P = args.P or cfg["P"]
     model = {"v2": L.MODEL_V2, "groups": L.MODEL_GROUPS, "hs": L.MODEL_HORSESHOE}[cfg["model"]]
-    Bsz = args.block_size or (128 if model in (L.MODEL_HORSESHOE, L.MODEL_GROUPS) else 512)  # = libbrr's automatic B
+    Bsz = args.block_size or (128 if model in (L.MODEL_HORSESHOE, L.MODEL_GROUPS) or N < 32768 else 512)  # = libbrr's automatic B
     G = cfg["groups"]
     K = 1 if model == L.MODEL_HORSESHOE else len(CVA) + 1
     F = 1 if model == L.MODEL_GROUPS else 0
     x2 = args.x_storage == "2bit"
+    order_mode = L.ORDER_REFERENCE if args.order == "reference" else L.ORDER_BLOCKED
     rows = args.shard == "rows" and world > 1
     if rows:
         # exact row shards: rows [r0, r1) of the cohort, every marker
         r0, r1 = N * rank // world, N * (rank + 1) // world
         c0, c1, Pl, Nl = 0, P, P, r1 - r0
         s = B.Session(model, Nl, P, K=K, groups=G, F=F, device=local_rank, block_size=Bsz,
-                      order_mode=L.ORDER_BLOCKED, row_shard_rank=rank, row_shard_count=world, row_offset=r0,
+                      order_mode=order_mode, row_shard_rank=rank, row_shard_count=world, row_offset=r0,
                       N_total=N, x_storage=L.X_2BIT if x2 else L.X_F32)
     else:
         # contiguous block shards
@@ -385,7 +389,7 @@ def main():
         c0, c1 = b0 * Bsz, min(P, b1 * Bsz)
         Pl, Nl = c1 - c0, N
         s = B.Session(model, N, Pl, K=K, groups=G, F=F, M_total=P, col_offset=c0, device=local_rank,
-                      block_size=Bsz, order_mode=L.ORDER_BLOCKED, shard_rank=rank, shard_count=world,
+                      block_size=Bsz, order_mode=order_mode, shard_rank=rank, shard_count=world,
                       x_storage=L.X_2BIT if x2 else L.X_F32)
     # algorithmic bytes of one pass over this shard's genotypes (f32 values, or 2-bit codes + the
     # 16-B value table of every column)
@@ -549,7 +553,7 @@ def main():
                      + ("2-bit codes + f32 value tables" if x2 else "f32 X") + ", f64 arithmetic)"),
             "config": {"workload": cfg["workload"] + (" [2-bit genotype storage, SURVEY 8f3]" if x2 else ""),
                        "x_storage": args.x_storage, "N": N, "P": P, "K": K, "groups": G,
-                       "block_size": Bsz, "order": "blocked", "fused_stream_wg": int(s.scalar(104)), "code_cache": int(s.scalar(105)), "pipeline_lag": int(s.scalar(106)),
+                       "block_size": Bsz, "order": args.order, "fused_stream_wg": int(s.scalar(104)), "code_cache": int(s.scalar(105)), "pipeline_lag": int(s.scalar(106)),
                        "parallelism": f"row-shard x{world} (exact)" if rows else f"column-shard x{world}",
                        "setup_s": round(t_setup, 2), "diag": diag,
                        **({"output": emit} if emit else {})},
