@@ -2145,7 +2145,9 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
   const bool lcopy = XF && lsrc != nullptr && t < d.B;
   const float4 lval = (lcopy && t < lcnt) ? lsrc[t] : make_float4(0.f, 0.f, 0.f, 0.f);
   double *s_pd = s_pbo;  // b_old - b_new per list entry
-  (void)s_pbn;
+  // 2-bit: per entry the offset of its code byte at row quad 0 -- in the LDS code cache (tiles of
+  // this workgroup's rows) or in the HBM code tiles -- so a lane adds only its quad
+  int64_t *s_cb = reinterpret_cast<int64_t *>(s_pbn);
   if (t < 64) {
     const int np = ld_sc1_int(d.pend_n + slot);
     const int nr = ld_sc1_int(d.pend_n + NSLOT + slot);  // entries before the neutral padding
@@ -2155,8 +2157,13 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
       // neutral padding entries (b_old = b_new = 0) load the last real column again: a cache
       // hit instead of column 0 from HBM, and no branch in the batched loads
       const int es = e < nr ? e : max(nr - 1, 0);
-      s_pidx[e] = ld_sc1_int(pidx + es);
-      if (XF) s_ppos[e] = ld_sc1_int(d.pend_gi + slot * d.pend_stride + es);  // in-block (storage) index
+      const int col = ld_sc1_int(pidx + es);
+      s_pidx[e] = col;
+      if (XF) {
+        const int gi = ld_sc1_int(d.pend_gi + slot * d.pend_stride + es);  // in-block (storage) index
+        s_ppos[e] = gi;
+        s_cb[e] = ccode ? (int64_t)(gi >> 4) * (npass * 64 * 16) + (gi & 15) : code_off(col, 0, d.B, d.ldc);
+      }
       s_pd[e] = ld_sc1(pbo + e) - ld_sc1(pbn + e);
     }
     if (lane == 0) s_np[0] = np;
@@ -2174,18 +2181,55 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
       const bool ok = r0 + off < r1;
       const int64_t src = ok ? r0 + off : r0;  // lanes past the rows re-read row r0 (not stored)
       auto xload = [&](int e) __attribute__((always_inline)) -> float4 {
-        if constexpr (XF) {
-          // code byte of (column, this lane's row quad): from the LDS code cache (tiles of this
-          // workgroup's rows, stream_role) or the HBM code tiles
-          const int gi = s_ppos[e];
-          const uint32_t byte = ccode ? (uint32_t)ccode[((gi >> 4) * (npass * 64) + (off >> 2)) * 16 + (gi & 15)]
-                                      : (uint32_t)d.Xc[code_off(s_pidx[e], src >> 2, d.B, d.ldc)];
-          return x_decode4(byte, lutb[gi]);
-        } else {
-          return ldg4(d.X + (int64_t)s_pidx[e] * d.ld + src);
-        }
+        return ldg4(d.X + (int64_t)s_pidx[e] * d.ld + src);
       };
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      if constexpr (XF) {
+        // 2-bit: raw code bytes in flight (2 batches of AB), decoded when consumed; the byte of
+        // (entry e, this lane's quad) from LDS or HBM in separate loops (concrete address spaces)
+        auto run = [&](auto lds_c) __attribute__((always_inline)) {
+          constexpr bool LDSC = decltype(lds_c)::value;
+          const int64_t qo = LDSC ? (int64_t)(off >> 2) * 16 : (src >> 2) * 16;
+          auto rload = [&](int e) __attribute__((always_inline)) -> uint32_t {
+            if constexpr (LDSC)
+              return ((const __attribute__((address_space(3))) uint8_t *)ccode)[s_cb[e] + qo];
+            else
+              return d.Xc[s_cb[e] + qo];
+          };
+          uint32_t ra[AB], rb[AB];
+          auto consume = [&](const uint32_t (&r)[AB], int e) __attribute__((always_inline)) {
+#pragma unroll
+            for (int q = 0; q < AB; ++q) {
+              if (e + q < e1) {
+                const float4 x = x_decode4(r[q], lutb[s_ppos[e + q]]);
+                const double dd = s_pd[e + q];
+                a0 += (double)x.x * dd;
+                a1 += (double)x.y * dd;
+                a2 += (double)x.z * dd;
+                a3 += (double)x.w * dd;
+              }
+            }
+          };
+#pragma unroll
+          for (int q = 0; q < AB; ++q) ra[q] = rload(min(e0 + q, e1 - 1));
+          for (int e = e0; e < e1; e += 2 * AB) {
+            const bool more = e + AB < e1;
+            if (more) {
+#pragma unroll
+              for (int q = 0; q < AB; ++q) rb[q] = rload(min(e + AB + q, e1 - 1));
+            }
+            consume(ra, e);
+            if (!more) break;
+            if (e + 2 * AB < e1) {
+#pragma unroll
+              for (int q = 0; q < AB; ++q) ra[q] = rload(min(e + 2 * AB + q, e1 - 1));
+            }
+            consume(rb, e + AB);
+          }
+        };
+        if (ccode) run(std::true_type{});
+        else run(std::false_type{});
+      } else {
       float4 xa[AB], xb[AB];
       auto consume = [&](const float4 (&x)[AB], int e) __attribute__((always_inline)) {
 #pragma unroll
@@ -2214,6 +2258,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
           for (int q = 0; q < AB; ++q) xa[q] = xload(min(e + 2 * AB + q, e1 - 1));
         }
         consume(xb, e + AB);
+      }
       }
       if (G == 1) {
         if (ok) {
@@ -2929,7 +2974,7 @@ hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipS
   if (!fn) return hipErrorInvalidValue;
   Dev dd = d;
   if (const char *ex = getenv("BRR_TEST_CENSUS_EXTRA")) dd.abase += atoi(ex);
-  int nslot = c.nslot, nsg = c.nsg, rpw = c.rpw, npass = c.npass, nred = c.nred, cc = d.Xc ? c.ccache : 0;
+  int nslot = c.nslot, nsg = c.nsg, rpw = c.rpw, npass = c.npass, nred = c.nred, cc = c.ccache;
   void *args[] = {&dd, &it, &nslot, &nsg, &rpw, &npass, &nred, &cc};
   return hipLaunchCooperativeKernel(fn, dim3((unsigned)(c.nsg + 1 + c.nred)), dim3(SWEEP_NT), args,
                                     (unsigned)c.lds, st);

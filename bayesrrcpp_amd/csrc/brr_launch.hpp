@@ -34,7 +34,7 @@ hipError_t launch_group_sum(const GroupPtrs &p, int64_t n, hipStream_t st);
 hipError_t launch_prep(const Dev &d, uint32_t it, hipStream_t st);
 struct FusedCfg {
   int nsg = 0, rpw = 0, npass = 0, nslot = 0, ngroups = 0, nred = 0;
-  int ccache = 0;  // 2-bit storage: the streamers keep the last three blocks' code bytes in LDS
+  int ccache = 0;  // 2-bit storage: the streamers keep the last blocks' code tiles in LDS
   size_t lds = 0;
 };
 bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg);
