@@ -323,8 +323,10 @@ __global__ void k_copy_f32(const float *src, int64_t lds, float *dst, int64_t ld
 // Block Gram matrices: G[b][i][j] = sum_r x(col(b,i))[r] * x(col(b2,j))[r] in f64 with
 // b2 = (b + shift) mod nb: shift 0 gives the diagonal blocks X_b^T X_b, shift 1 the cross-Gram
 // of cycle neighbours (also stored transposed in GT when GT != nullptr).  64x64 output tile per
-// workgroup, 4x4 per thread, 64-row chunks staged in LDS.  Element (i,j) and (j,i) of a
-// diagonal block accumulate identical products in identical order -> exactly symmetric.
+// workgroup (a 32 x 32 quadrant per wave, 2 x 2 tiles of the FP64 matrix core's 16 x 16 x 4 op),
+// 64-row chunks staged in LDS as f32 (the genotype values), converted to f64 as operands.  The
+// f32 x f32 products are exact in f64; element (i,j) and (j,i) of a diagonal block accumulate the
+// same products in the same k order.
 __global__ __launch_bounds__(256) void k_gram(Dev d, const int *member, const int *bsz, int B, int nb, int shift,
                                               double *G, double *GT) {
   const float *X = d.X;
@@ -337,12 +339,14 @@ __global__ __launch_bounds__(256) void k_gram(Dev d, const int *member, const in
   const int ti = blockIdx.y / ntile, tj = blockIdx.y % ntile;
   const int bs = bsz[gb], bs2 = bsz[gb2];
   const int t = threadIdx.x;
-  const int ty = t >> 4, tx = t & 15;
-  double acc[4][4];
+  const int lane = t & 63, wv = t >> 6;
+  const int wi = wv >> 1, wj = wv & 1;  // this wave's 32 x 32 quadrant of the 64 x 64 tile
+  typedef double f64x4 __attribute__((ext_vector_type(4)));
+  f64x4 acc[2][2];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+    for (int b = 0; b < 2; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
   // loader: column c = t >> 2 (0..63), rows (t & 3) * 16 .. +16
   const int lc = t >> 2, lr = (t & 3) * 16;
   const int ci = ti * 64 + lc, cj = tj * 64 + lc;
@@ -367,31 +371,42 @@ __global__ __launch_bounds__(256) void k_gram(Dev d, const int *member, const in
       Bs[lr + q + 0][lc] = vb.x; Bs[lr + q + 1][lc] = vb.y; Bs[lr + q + 2][lc] = vb.z; Bs[lr + q + 3][lc] = vb.w;
     }
     __syncthreads();
+    // 16 steps of v_mfma_f64_16x16x4_f64 over the chunk's 64 rows: lane l supplies A[i = l&15]
+    // [k = l>>4] = x(col i0 + i)[row k] and B[k][j = l&15] = x(col j0 + j)[row k] (f32 values,
+    // exact in f64); the products are exact and accumulated in f64
 #pragma unroll 4
-    for (int r = 0; r < 64; ++r) {
-      double a[4], b[4];
+    for (int kb = 0; kb < 64; kb += 4) {
+      const int k = kb + (lane >> 4);
+      double a[2], b[2];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) { a[q] = (double)As[r][ty * 4 + q]; b[q] = (double)Bs[r][tx * 4 + q]; }
+      for (int q = 0; q < 2; ++q) {
+        a[q] = (double)As[k][wi * 32 + q * 16 + (lane & 15)];
+        b[q] = (double)Bs[k][wj * 32 + q * 16 + (lane & 15)];
+      }
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
+      for (int p = 0; p < 2; ++p)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[p][q] = fma(a[p], b[q], acc[p][q]);
+        for (int q = 0; q < 2; ++q) acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[p], b[q], acc[p][q], 0, 0, 0);
     }
     __syncthreads();
   }
   double *g = G + (int64_t)gb * B * B;
   double *gt = GT ? GT + (int64_t)gb * B * B : nullptr;
+  // C/D map of the f64 MFMA: element r of lane l is (row (l>>4) + 4 r, column l&15) of the tile
 #pragma unroll
-  for (int p = 0; p < 4; ++p)
+  for (int p = 0; p < 2; ++p)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int i = ti * 64 + ty * 4 + p, jj = tj * 64 + tx * 4 + q;
-      if (i < B && jj < B) {
-        const double v = (i < bs && jj < bs2) ? acc[p][q] : 0.0;
-        g[(int64_t)i * B + jj] = v;
-        if (gt) gt[(int64_t)jj * B + i] = v;
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = ti * 64 + wi * 32 + p * 16 + (lane >> 4) + 4 * r;
+        const int jj = tj * 64 + wj * 32 + q * 16 + (lane & 15);
+        if (i < B && jj < B) {
+          const double v = (i < bs && jj < bs2) ? acc[p][q][r] : 0.0;
+          g[(int64_t)i * B + jj] = v;
+          if (gt) gt[(int64_t)jj * B + i] = v;
+        }
       }
-    }
 }
 
 __global__ void k_xsq_from_gram(const double *G, const int *member, const int *bsz, int B, int nb,
@@ -2976,6 +2991,12 @@ hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipS
   if (const char *ex = getenv("BRR_TEST_CENSUS_EXTRA")) dd.abase += atoi(ex);
   int nslot = c.nslot, nsg = c.nsg, rpw = c.rpw, npass = c.npass, nred = c.nred, cc = c.ccache;
   void *args[] = {&dd, &it, &nslot, &nsg, &rpw, &npass, &nred, &cc};
+  // BRR_PLAIN_LAUNCH=1: a plain launch of the same kernel (the census then guards residency alone).
+  // Used for rocprofv3 runs: with ROCm 7.2's rocprofv3 attached, a process that made a cooperative
+  // launch segfaults in its exit handlers (after the profile is written); without the tool it exits
+  // cleanly (scripts/gpu_exitcrash.sh).
+  static const bool plain = getenv("BRR_PLAIN_LAUNCH") && getenv("BRR_PLAIN_LAUNCH")[0] == '1';
+  if (plain) return hipLaunchKernel(fn, dim3((unsigned)(c.nsg + 1 + c.nred)), dim3(SWEEP_NT), args, (unsigned)c.lds, st);
   return hipLaunchCooperativeKernel(fn, dim3((unsigned)(c.nsg + 1 + c.nred)), dim3(SWEEP_NT), args,
                                     (unsigned)c.lds, st);
 }

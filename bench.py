@@ -560,6 +560,8 @@ def main():
             "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    s.synchronize()
+    s.close()  # device resources released while the runtime (and a profiler's tool) is still up
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -8,6 +8,9 @@ set -o pipefail
 mkdir -p gpurun_out
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
+# rocprofv3 + cooperative launch: segfault at process exit (tool teardown); profile the plain
+# launch of the same kernel
+export BRR_PLAIN_LAUNCH=1
 TAG=${TAG:-prof}
 ARGS="--config ${CONFIG:-c2} --x-storage ${XS:-f32} --no-cpu-baseline ${BENCH_ARGS}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_trace -o run --output-format csv \
