@@ -190,7 +190,7 @@ def pmc_traffic(args, N, P, B, fused, x_bytes):
     same configuration (profiles/*_pmc.json, written by scripts/pmc_json.py: FETCH_SIZE x2 +
     WRITE_SIZE, gfx950 correction), or None."""
     import glob
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json"))):
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")), reverse=True):  # newest round first
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
