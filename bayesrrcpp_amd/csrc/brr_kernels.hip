@@ -320,73 +320,93 @@ __global__ void k_copy_f32(const float *src, int64_t lds, float *dst, int64_t ld
 }
 
 // ------------------------------------------------------------------------------------
+#ifndef GRAM_TILE
+#define GRAM_TILE 128
+#endif
+#ifndef GRAM_KC
+#define GRAM_KC 128
+#endif
+constexpr size_t GRAM_LDS = 2 * sizeof(float) * GRAM_KC * (GRAM_TILE + 1);
 // Block Gram matrices: G[b][i][j] = sum_r x(col(b,i))[r] * x(col(b2,j))[r] in f64 with
 // b2 = (b + shift) mod nb: shift 0 gives the diagonal blocks X_b^T X_b, shift 1 the cross-Gram
-// of cycle neighbours (also stored transposed in GT when GT != nullptr).  64x64 output tile per
-// workgroup (a 32 x 32 quadrant per wave, 2 x 2 tiles of the FP64 matrix core's 16 x 16 x 4 op),
-// 64-row chunks staged in LDS as f32 (the genotype values), converted to f64 as operands.  The
+// of cycle neighbours (also stored transposed in GT when GT != nullptr).  GRAM_TILE^2 output tile
+// per workgroup (a quadrant per wave in 16 x 16 tiles of the FP64 matrix core's 16 x 16 x 4 op),
+// 32-row chunks staged in LDS as f32 (the genotype values), converted to f64 as operands.  The
 // f32 x f32 products are exact in f64; element (i,j) and (j,i) of a diagonal block accumulate the
 // same products in the same k order.
 __global__ __launch_bounds__(256) void k_gram(Dev d, const int *member, const int *bsz, int B, int nb, int shift,
                                               double *G, double *GT) {
+  constexpr int T = GRAM_TILE;  // output tile T x T per workgroup, a (T/2) x (T/2) quadrant per wave
+  constexpr int KC = GRAM_KC;   // rows per LDS chunk (512 B per column: DRAM page locality)
+  constexpr int NQ = T / 32;    // 16 x 16 MFMA tiles per wave and dimension
   const float *X = d.X;
   const int64_t ld = d.ld;
-  __shared__ float As[64][65];
-  __shared__ float Bs[64][65];
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  float (*As)[T + 1] = reinterpret_cast<float (*)[T + 1]>(gsm);
+  float (*Bs)[T + 1] = reinterpret_cast<float (*)[T + 1]>(gsm + sizeof(float) * KC * (T + 1));
   const int gb = blockIdx.x;
   const int gb2 = (gb + shift) % nb;
-  const int ntile = (B + 63) / 64;
+  const int ntile = (B + T - 1) / T;
   const int ti = blockIdx.y / ntile, tj = blockIdx.y % ntile;
   const int bs = bsz[gb], bs2 = bsz[gb2];
   const int t = threadIdx.x;
   const int lane = t & 63, wv = t >> 6;
-  const int wi = wv >> 1, wj = wv & 1;  // this wave's 32 x 32 quadrant of the 64 x 64 tile
+  const int wi = wv >> 1, wj = wv & 1;  // this wave's quadrant of the tile
   typedef double f64x4 __attribute__((ext_vector_type(4)));
-  f64x4 acc[2][2];
+  f64x4 acc[NQ][NQ];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < NQ; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
-  // loader: column c = t >> 2 (0..63), rows (t & 3) * 16 .. +16
-  const int lc = t >> 2, lr = (t & 3) * 16;
-  const int ci = ti * 64 + lc, cj = tj * 64 + lc;
-  const int64_t ca = (ci < bs) ? member[(int64_t)gb * B + ci] : -1;
-  const int64_t cb = (cj < bs2) ? member[(int64_t)gb2 * B + cj] : -1;
-  const float *pa = (ca >= 0 && X) ? X + ca * ld : nullptr;
-  const float *pb = (cb >= 0 && X) ? X + cb * ld : nullptr;
+    for (int b = 0; b < NQ; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
+  // loader: the chunk's KC rows of the tile's T columns of each operand, in (column, row quad)
+  // elements with consecutive threads on consecutive quads of one column (a wave reads KC / 4 x
+  // 16 B = 512 B contiguous per column); the columns' global indices staged once in LDS
+  __shared__ int64_t s_ca[T], s_cb[T];
+  __shared__ float4 s_la[T], s_lb[T];
+  for (int c = t; c < T; c += 256) {
+    const int ci = ti * T + c, cj = tj * T + c;
+    s_ca[c] = ci < bs ? member[(int64_t)gb * B + ci] : -1;
+    s_cb[c] = cj < bs2 ? member[(int64_t)gb2 * B + cj] : -1;
+    const float4 z = make_float4(0, 0, 0, 0);
+    s_la[c] = (s_ca[c] >= 0 && d.Xc) ? x_lut(d, s_ca[c]) : z;
+    s_lb[c] = (s_cb[c] >= 0 && d.Xc) ? x_lut(d, s_cb[c]) : z;
+  }
+  __syncthreads();
+  constexpr int QPC = KC / 4;  // row quads per column and chunk
   const float4 z4 = make_float4(0, 0, 0, 0);
-  const float4 la = (ca >= 0 && d.Xc) ? x_lut(d, ca) : z4, lb = (cb >= 0 && d.Xc) ? x_lut(d, cb) : z4;
-  for (int64_t r0 = 0; r0 < ld; r0 += 64) {
-#pragma unroll
-    for (int q = 0; q < 16; q += 4) {
+  for (int64_t r0 = 0; r0 < ld; r0 += KC) {
+#pragma unroll 4
+    for (int e = t; e < T * QPC; e += 256) {
+      const int c = e / QPC, rq = (e - c * QPC) * 4;
+      const int64_t ca = s_ca[c], cb = s_cb[c];
       float4 va, vb;
       if (d.Xc) {  // 2-bit codes: the same f32 values, decoded
-        va = ca >= 0 ? x_decode4(d.Xc[code_off(ca, (r0 + lr + q) >> 2, d.B, d.ldc)], la) : z4;
-        vb = cb >= 0 ? x_decode4(d.Xc[code_off(cb, (r0 + lr + q) >> 2, d.B, d.ldc)], lb) : z4;
+        va = ca >= 0 ? x_decode4(d.Xc[code_off(ca, (r0 + rq) >> 2, d.B, d.ldc)], s_la[c]) : z4;
+        vb = cb >= 0 ? x_decode4(d.Xc[code_off(cb, (r0 + rq) >> 2, d.B, d.ldc)], s_lb[c]) : z4;
       } else {
-        va = pa ? *reinterpret_cast<const float4 *>(pa + r0 + lr + q) : z4;
-        vb = pb ? *reinterpret_cast<const float4 *>(pb + r0 + lr + q) : z4;
+        va = ca >= 0 ? *reinterpret_cast<const float4 *>(X + ca * ld + r0 + rq) : z4;
+        vb = cb >= 0 ? *reinterpret_cast<const float4 *>(X + cb * ld + r0 + rq) : z4;
       }
-      As[lr + q + 0][lc] = va.x; As[lr + q + 1][lc] = va.y; As[lr + q + 2][lc] = va.z; As[lr + q + 3][lc] = va.w;
-      Bs[lr + q + 0][lc] = vb.x; Bs[lr + q + 1][lc] = vb.y; Bs[lr + q + 2][lc] = vb.z; Bs[lr + q + 3][lc] = vb.w;
+      As[rq + 0][c] = va.x; As[rq + 1][c] = va.y; As[rq + 2][c] = va.z; As[rq + 3][c] = va.w;
+      Bs[rq + 0][c] = vb.x; Bs[rq + 1][c] = vb.y; Bs[rq + 2][c] = vb.z; Bs[rq + 3][c] = vb.w;
     }
     __syncthreads();
-    // 16 steps of v_mfma_f64_16x16x4_f64 over the chunk's 64 rows: lane l supplies A[i = l&15]
-    // [k = l>>4] = x(col i0 + i)[row k] and B[k][j = l&15] = x(col j0 + j)[row k] (f32 values,
-    // exact in f64); the products are exact and accumulated in f64
-#pragma unroll 4
-    for (int kb = 0; kb < 64; kb += 4) {
+    // v_mfma_f64_16x16x4_f64 over the chunk's rows, 4 per step: lane l supplies A[i = l&15]
+    // [k = l>>4] = x(col i)[row k] and B[k][j = l&15] = x(col j)[row k] (f32 values, exact in
+    // f64); the products are exact and accumulated in f64
+#pragma unroll 2
+    for (int kb = 0; kb < KC; kb += 4) {  // (KC rows)
       const int k = kb + (lane >> 4);
-      double a[2], b[2];
+      double a[NQ], b[NQ];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        a[q] = (double)As[k][wi * 32 + q * 16 + (lane & 15)];
-        b[q] = (double)Bs[k][wj * 32 + q * 16 + (lane & 15)];
+      for (int q = 0; q < NQ; ++q) {
+        a[q] = (double)As[k][wi * (T / 2) + q * 16 + (lane & 15)];
+        b[q] = (double)Bs[k][wj * (T / 2) + q * 16 + (lane & 15)];
       }
 #pragma unroll
-      for (int p = 0; p < 2; ++p)
+      for (int p = 0; p < NQ; ++p)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[p], b[q], acc[p][q], 0, 0, 0);
+        for (int q = 0; q < NQ; ++q) acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[p], b[q], acc[p][q], 0, 0, 0);
     }
     __syncthreads();
   }
@@ -394,13 +414,13 @@ __global__ __launch_bounds__(256) void k_gram(Dev d, const int *member, const in
   double *gt = GT ? GT + (int64_t)gb * B * B : nullptr;
   // C/D map of the f64 MFMA: element r of lane l is (row (l>>4) + 4 r, column l&15) of the tile
 #pragma unroll
-  for (int p = 0; p < 2; ++p)
+  for (int p = 0; p < NQ; ++p)
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < NQ; ++q)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int i = ti * 64 + wi * 32 + p * 16 + (lane >> 4) + 4 * r;
-        const int jj = tj * 64 + wj * 32 + q * 16 + (lane & 15);
+        const int i = ti * T + wi * (T / 2) + p * 16 + (lane >> 4) + 4 * r;
+        const int jj = tj * T + wj * (T / 2) + q * 16 + (lane & 15);
         if (i < B && jj < B) {
           const double v = (i < bs && jj < bs2) ? acc[p][q][r] : 0.0;
           g[(int64_t)i * B + jj] = v;
@@ -2836,9 +2856,12 @@ hipError_t launch_cast_x(const void *src, bool is_f64, int64_t lds, float *dst, 
 }
 
 hipError_t launch_gram(const Dev &d, int shift, double *G, double *GT, hipStream_t st) {
-  const int nt = (d.B + 63) / 64;
-  hipLaunchKernelGGL(k_gram, dim3((unsigned)d.nb, (unsigned)(nt * nt)), dim3(256), 0, st, d, d.member, d.bsz, d.B,
-                     d.nb, shift, G, GT);
+  const int nt = (d.B + GRAM_TILE - 1) / GRAM_TILE;
+  static const hipError_t attr = hipFuncSetAttribute((const void *)k_gram, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)GRAM_LDS);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL(k_gram, dim3((unsigned)d.nb, (unsigned)(nt * nt)), dim3(256), GRAM_LDS, st, d, d.member, d.bsz,
+                     d.B, d.nb, shift, G, GT);
   return hipGetLastError();
 }
 
