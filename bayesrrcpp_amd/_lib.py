@@ -47,7 +47,7 @@ EXPORTED = [
     "brr_session_set_restart", "brr_session_set_pi", "brr_session_init", "brr_session_sweep",
     "brr_session_exchange_sizes", "brr_session_set_exchange", "brr_session_exchange_buffers",
     "brr_session_exchange_copy", "brr_comm_unique_id", "brr_session_comm_init",
-    "brr_session_sweep_local",
+    "brr_session_sweep_local", "brr_session_init_local", "brr_session_init_finish",
     "brr_session_sweep_finish", "brr_session_get_scalar", "brr_session_get_vector",
     "brr_session_set_vector", "brr_session_set_scalar", "brr_session_iteration",
     "brr_session_set_timing", "brr_session_timing", "brr_session_block_size",
@@ -115,6 +115,8 @@ def lib():
     L.brr_comm_unique_id.argtypes = [C.c_char_p]
     L.brr_session_comm_init.argtypes = [vp, C.c_char_p, C.c_int32, C.c_int32]
     L.brr_session_sweep_local.argtypes = [vp]
+    L.brr_session_init_local.argtypes = [vp, C.c_int32]
+    L.brr_session_init_finish.argtypes = [vp]
     L.brr_session_sweep_finish.argtypes = [vp]
     L.brr_session_get_scalar.argtypes = [vp, C.c_int32, D]
     L.brr_session_get_vector.restype = C.c_int64

@@ -145,6 +145,7 @@ struct brr_session {
   int rshard = 0, nrshard = 1;  // exact row shards: this session's rank / count
   hipEvent_t ev_x = nullptr;    // row shards in one process (brr_group): cross-stream ordering
   int32_t iteration = 0;
+  bool init_pending = false;  // column-shard restart between init_local and init_finish
   bool initialized = false, pi_given = false, need_reduce = false, have_y = false, have_x = false;
   bool x2bit = false;  // genotype storage: 2-bit codes (opt.x_storage == BRR_X_2BIT)
   double mu0 = 0, sigmaE0 = 0;
@@ -500,6 +501,17 @@ int coll_grams(Coll &c) {
   return coll_sum(c, [](brr_session *s) { return s->d.xgramT; }, nbb);
 }
 
+// last init step: hyper-parameter init draws from the (summed) statistics
+int init_finish(brr_session *s, const double *stats) {
+  HIPCHK(launch_hyper_init(s->d, stats, s->pi_given, s->st));
+  HIPCHK(hipStreamSynchronize(s->st));
+  s->iteration = 0;
+  s->initialized = true;
+  s->init_pending = false;
+  s->need_reduce = false;
+  return 0;
+}
+
 int coll_init(Coll &c, int32_t seed) {
   for (brr_session *s : c.ss) {
     if (!s->have_x) { set_error("X not uploaded"); return -1; }
@@ -539,16 +551,25 @@ int coll_init(Coll &c, int32_t seed) {
   if (int rc = coll_sum(c, sc_sums, 2)) return rc;
   return coll_each(c, [](brr_session *s) -> int {
     Dev &d = s->d;
+    const double *stats = d.stats;
     if (s->model == MODEL_RESTART) {
-      if (s->nshard > 1) { set_error("restart across column shards needs summed counts: not supported"); return -1; }
-      HIPCHK(launch_markers(d, H_MR_COUNT_ALL, 0, s->st));  // every row shard holds every marker
+      // v(g, k) counts over every marker (BRv2Grstart.cpp:157-165): a row shard holds every
+      // marker; column shards sum their local counts across shards first
+      HIPCHK(launch_markers(d, H_MR_COUNT_ALL, 0, s->st));
+      if (s->nshard > 1) {
+        if (int rc = brr_session_exchange_buffers(s, nullptr, nullptr)) return rc;
+        HIPCHK(hipMemcpyAsync(s->ex_stats, d.stats, sizeof(double) * s->NS, hipMemcpyDeviceToDevice, s->st));
+        if (!s->comm) {  // brr_session_init_local: the caller sums the exchange statistics
+          HIPCHK(hipStreamSynchronize(s->st));
+          s->init_pending = true;
+          return 0;
+        }
+        ncclResult_t r = ncclAllReduce(s->ex_stats, s->ex_stats, (size_t)s->NS, ncclDouble, ncclSum, s->comm, s->st);
+        if (r != ncclSuccess) { set_error("ncclAllReduce failed: %s", ncclGetErrorString(r)); return -2; }
+        stats = s->ex_stats;
+      }
     }
-    HIPCHK(launch_hyper_init(d, d.stats, s->pi_given, s->st));
-    HIPCHK(hipStreamSynchronize(s->st));
-    s->iteration = 0;
-    s->initialized = true;
-    s->need_reduce = false;
-    return 0;
+    return init_finish(s, stats);
   });
 }
 
@@ -1262,8 +1283,28 @@ int brr_session_set_pi(brr_session *s, const double *pi) {
 
 int brr_session_init(brr_session *s, int32_t seed) {
   if (!s) return -1;
+  if (s->model == MODEL_RESTART && s->nshard > 1 && !s->comm) {
+    set_error("restart across column shards sums the component counts at init: brr_session_comm_init "
+              "first, or drive brr_session_init_local / exchange / brr_session_init_finish yourself");
+    return -1;
+  }
   Coll c{{s}};
   return coll_init(c, seed);
+}
+
+int brr_session_init_local(brr_session *s, int32_t seed) {
+  if (!s) return -1;
+  if (s->comm) { set_error("init_local is for sessions without a communicator: use brr_session_init"); return -1; }
+  Coll c{{s}};
+  return coll_init(c, seed);
+}
+
+int brr_session_init_finish(brr_session *s) {
+  if (!s) return -1;
+  if (s->initialized) return 0;  // nothing was left to sum (not a column-sharded restart)
+  if (!s->init_pending) { set_error("brr_session_init_local has not run"); return -1; }
+  HIPCHK(hipSetDevice(s->device));
+  return init_finish(s, s->ex_stats);
 }
 
 int brr_session_sweep(brr_session *s, int32_t n) {

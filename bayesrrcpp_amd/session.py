@@ -128,6 +128,16 @@ class Session:
         L.check(L.lib().brr_session_sweep(self.h, n), "sweep")
         return self
 
+    def init_local(self, seed=1):
+        """Column-sharded init without a communicator: sum exchange_get()[1] across shards,
+        exchange_set(None, total), then init_finish() (restart model; a full init otherwise)."""
+        L.check(L.lib().brr_session_init_local(self.h, seed), "init_local")
+        return self
+
+    def init_finish(self):
+        L.check(L.lib().brr_session_init_finish(self.h), "init_finish")
+        return self
+
     def exchange_sizes(self):
         a, b = C.c_int64(), C.c_int64()
         L.check(L.lib().brr_session_exchange_sizes(self.h, C.byref(a), C.byref(b)), "exchange_sizes")
@@ -149,9 +159,10 @@ class Session:
         return e, st
 
     def exchange_set(self, eps, stats):
-        e = np.ascontiguousarray(eps, dtype=np.float64)
-        st = np.ascontiguousarray(stats, dtype=np.float64)
-        L.check(L.lib().brr_session_exchange_copy(self.h, 1, _d(e), _d(st)), "exchange_copy")
+        e = None if eps is None else np.ascontiguousarray(eps, dtype=np.float64)
+        st = None if stats is None else np.ascontiguousarray(stats, dtype=np.float64)
+        L.check(L.lib().brr_session_exchange_copy(self.h, 1, None if e is None else _d(e),
+                                                  None if st is None else _d(st)), "exchange_copy")
 
     def comm_init(self, unique_id: bytes, nranks: int, rank: int):
         L.check(L.lib().brr_session_comm_init(self.h, unique_id, nranks, rank), "comm_init")

@@ -180,6 +180,13 @@ int brr_session_exchange_buffers(brr_session *s, double **dev_eps, double **dev_
 int brr_session_exchange_copy(brr_session *s, int32_t dir, double *host_eps, double *host_stats);
 int brr_session_sweep_local(brr_session *s);
 int brr_session_sweep_finish(brr_session *s);
+/* the same split for init, needed by the restart model only (its pi init counts every
+ * marker's component, src/BRv2Grstart.cpp:157-165): brr_session_init_local(s, seed) leaves
+ * this shard's counts in the exchange statistics; the caller sums them across shards (as for a
+ * sweep) and calls brr_session_init_finish(s).  For every other model init_local is a complete
+ * init and init_finish a no-op.  With a communicator, brr_session_init does all of it. */
+int brr_session_init_local(brr_session *s, int32_t seed);
+int brr_session_init_finish(brr_session *s);
 
 /* native multi-GPU: RCCL over xGMI, one process per GPU.  Rank 0 creates the 128-byte id,
  * the caller broadcasts it (MPI, a file, torch.distributed/gloo ...), every rank calls

@@ -331,6 +331,62 @@ def test_sharded_two_sessions_match_oracle(brr, oracle_mod, require_gpu):
             assert _rel(s.vector(L.PI), orc.vector(O.V_PI)) < RTOL
 
 
+def test_restart_column_shards(brr, oracle_mod, require_gpu):
+    """Restart across two column shards: the pi init's component counts (BRv2Grstart.cpp:157-165)
+    summed across shards through init_local / exchange / init_finish, then the column-sharded
+    sweep, == the oracle's 2-shard emulation; a sharded restart without a communicator or the
+    split init is refused."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P, B, G = 260, 512, 128, 3
+    X, Y, _ = _cohort(O, N, P, n_causal=30)
+    gA = (np.arange(P) % G).astype(np.int32)
+    cva2 = np.tile(CVA, (G, 1))
+    prev = O.Oracle(O.GROUPS, X, Y, cva=cva2, G=G, gAssign=gA, seed=3, order_mode=0, block_size=B, **HYP)
+    prev.sweep(4)
+    st = dict(mu0=prev.scalar(O.S_MU), beta0=prev.vector(O.V_BETA), sigmaE0=prev.scalar(O.S_SIGMAE),
+              sigmaGG0=prev.vector(O.V_SIGMAGG), eps0=prev.vector(O.V_EPS), comp0=prev.vector(O.V_COMP))
+    sess = []
+    for r, c0 in enumerate((0, 256)):
+        s = brr.Session(L.MODEL_RESTART, N, 256, K=len(CVA) + 1, groups=G, M_total=P, col_offset=c0,
+                        block_size=B, shard_rank=r, shard_count=2)
+        s.upload_x(X[:, c0:c0 + 256])
+        s.set_bayesr(HYP["sigma0"], HYP["v0E"], HYP["s02E"], HYP["v0G"], HYP["s02G"], cva2, gA[c0:c0 + 256])
+        s.set_restart(st["mu0"], st["beta0"][c0:c0 + 256], st["sigmaE0"], st["sigmaGG0"], st["eps0"],
+                      st["comp0"][c0:c0 + 256])
+        sess.append(s)
+    with pytest.raises(RuntimeError, match="column shards"):
+        sess[0].init(11)
+    for s in sess:
+        s.init_local(11)
+    tot = sum(s.exchange_get()[1] for s in sess)
+    for s in sess:
+        s.exchange_set(None, tot)
+        s.init_finish()
+    orc = O.Oracle(O.RESTART, X, None, cva=cva2, G=G, gAssign=gA, seed=11, order_mode=0, block_size=B,
+                   N=N, n_shards=2, **HYP, **st)
+    for s in sess:
+        assert _rel(s.vector(L.PI), orc.vector(O.V_PI)) < RTOL  # Dirichlet(v + 1) of the summed counts
+    for it in range(4):
+        for s in sess:
+            s.sweep_local()
+        parts = [s.exchange_get() for s in sess]
+        te = parts[0][0] + parts[1][0]
+        ts = parts[0][1] + parts[1][1]
+        for s in sess:
+            s.exchange_set(te, ts)
+            s.sweep_finish()
+        orc.sweep(1)
+        comp = np.concatenate([s.vector(L.COMP) for s in sess])
+        assert np.array_equal(comp, orc.vector(O.V_COMP)), f"it={it}"
+        assert _rel(np.concatenate([s.vector(L.BETA) for s in sess]), orc.vector(O.V_BETA)) < RTOL
+        for s in sess:
+            assert _rel(s.vector(L.EPS), orc.vector(O.V_EPS)) < RTOL
+            assert _rel([s.scalar(L.SIGMAE)], [orc.scalar(O.S_SIGMAE)]) < RTOL
+            assert _rel(s.vector(L.PI), orc.vector(O.V_PI)) < RTOL
+            assert _rel(s.vector(L.SIGMAGG), orc.vector(O.V_SIGMAGG)) < RTOL
+
+
 def test_rccl_single_rank(brr, oracle_mod, require_gpu):
     """brr_session_comm_init + sweep with a 1-rank RCCL communicator runs the native path."""
     from bayesrrcpp_amd import _lib as L
