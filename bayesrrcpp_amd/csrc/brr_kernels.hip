@@ -2161,15 +2161,15 @@ constexpr int FUSED_GROUP = FUSED_GROUP_N;
 // ccode != nullptr (2-bit storage): the code bytes of the block being applied are in LDS
 // (stream_role's code cache, tiles [group][row quad][16]); s_ppos receives the in-block indices.
 // 2-bit storage: lsrc / ldst stage the next block's value tables (storage order, lcnt valid
-// entries) the same way; lutb = the value
-// tables of the block being applied (LDS, by visit position).
+// entries, f32 in HBM -> 4 doubles per column in LDS) the same way; lutb = the value tables of
+// the block being applied (LDS, 4 doubles per column, by visit position).
 template <int XF>
 __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0, int64_t r1, int npass,
                                               double *eps_l, int *s_pidx, double *s_pbo, double *s_pbn,
                                               int *s_np, double *s_part, const int *msrc = nullptr,
                                               int *mdst = nullptr, const uint8_t *ccode = nullptr,
                                               int *s_ppos = nullptr, const float4 *lsrc = nullptr,
-                                              float4 *ldst = nullptr, const float4 *lutb = nullptr, int lcnt = 0) {
+                                              double *ldst = nullptr, const double *lutb = nullptr, int lcnt = 0) {
 #pragma clang fp contract(off)
   constexpr int AB = 4;  // columns per batch (two batches in flight: 8 KiB per wave, 32 VGPRs, as many as the
                          // streaming ring leaves without spills)
@@ -2236,12 +2236,13 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
 #pragma unroll
             for (int q = 0; q < AB; ++q) {
               if (e + q < e1) {
-                const float4 x = x_decode4(r[q], lutb[s_ppos[e + q]]);
+                const double *lt = lutb + 4 * s_ppos[e + q];
+                const uint32_t b = r[q];
                 const double dd = s_pd[e + q];
-                a0 += (double)x.x * dd;
-                a1 += (double)x.y * dd;
-                a2 += (double)x.z * dd;
-                a3 += (double)x.w * dd;
+                a0 += lt[b & 3u] * dd;
+                a1 += lt[(b >> 2) & 3u] * dd;
+                a2 += lt[(b >> 4) & 3u] * dd;
+                a3 += lt[(b >> 6) & 3u] * dd;
               }
             }
           };
@@ -2328,7 +2329,10 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
     }
   }
   if (mcopy) mdst[t] = mval;
-  if (lcopy) ldst[t] = lval;
+  if (lcopy) {
+    double *l = ldst + 4 * t;
+    l[0] = lval.x; l[1] = lval.y; l[2] = lval.z; l[3] = lval.w;
+  }
   __syncthreads();
 }
 
@@ -2341,7 +2345,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
 // before the barrier that precedes the first item of the block.
 template <int CW, int P, int XF>
 __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int npass, double *eps_l, int *s_pidx,
-                                            double *s_pbo, double *s_pbn, int *s_np, float4 *s_lut, int *s_mem,
+                                            double *s_pbo, double *s_pbn, int *s_np, double *s_lut, int *s_mem,
                                             double *s_part, uint8_t *s_codes) {
 #pragma clang fp contract(off)
   const int t = threadIdx.x, lane = t & 63;
@@ -2355,12 +2359,18 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   const int LAG = d.lag;
   const int NLB = LAG + 3;  // value-table buffers: blocks s-1-LAG (apply) .. s+1 (staged)
   const int NCC = LAG + 2;  // code-cache buffers: blocks s-1-LAG (apply) .. s (being streamed)
-  auto lut_of = [&](int s) __attribute__((always_inline)) { return s_lut + (int64_t)(s % NLB) * B; };
+  // (a column's table: its 4 f32 values as doubles, read per value by code, so a product is the
+  // f32 path's (double) x * e without a decode or conversion)
+  auto lut_of = [&](int s) __attribute__((always_inline)) { return s_lut + (int64_t)(s % NLB) * B * 4; };
   auto stage_lut = [&](int s) __attribute__((always_inline)) {
     if constexpr (XF) {
       const int gb = d.gblk[s], bs = d.bsz[s];
       const float4 *src = reinterpret_cast<const float4 *>(d.xlut) + (int64_t)gb * B;
-      for (int i = t; i < B; i += SWEEP_NT) lut_of(s)[i] = i < bs ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int i = t; i < B; i += SWEEP_NT) {
+        const float4 l = i < bs ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        double *dl = lut_of(s) + 4 * i;
+        dl[0] = l.x; dl[1] = l.y; dl[2] = l.z; dl[3] = l.w;
+      }
     }
   };
   for (int i = t; i < npass * SROWS; i += SWEEP_NT) eps_l[i] = r0 + i < r1 ? d.eps[r0 + i] : 0.0;
@@ -2476,16 +2486,24 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
         reinterpret_cast<uint4 *>(s_codes)[((s % NCC) * (B >> 4) + ((w * CPW + c * CW) >> 4)) * (npass * 64) + p * 64 +
                                            lane] = xq[0][0];
     }
+    // one fused multiply-add per value into the column's accumulator, rows in order (the same
+    // operations on the same f64 values for both storages: the chains are identical)
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
-      float4 xv;
+      double x0, x1, x2, x3;
       if constexpr (XF) {
         const uint32_t word = j < 4 ? xq[0][0].x : (j < 8 ? xq[0][0].y : (j < 12 ? xq[0][0].z : xq[0][0].w));
-        xv = x_decode4((word >> (8 * (j & 3))) & 0xFFu, lut_of(s)[w * CPW + c * CW + j]);
+        const int sh = 8 * (j & 3);
+        const double *lt = lut_of(s) + 4 * (w * CPW + c * CW + j);
+        x0 = lt[__builtin_amdgcn_ubfe(word, sh, 2)];
+        x1 = lt[__builtin_amdgcn_ubfe(word, sh + 2, 2)];
+        x2 = lt[__builtin_amdgcn_ubfe(word, sh + 4, 2)];
+        x3 = lt[__builtin_amdgcn_ubfe(word, sh + 6, 2)];
       } else {
-        xv = xq[0][j];
+        const float4 xv = xq[0][j];
+        x0 = xv.x; x1 = xv.y; x2 = xv.z; x3 = xv.w;
       }
-      v[j] += (((double)xv.x * e0 + (double)xv.y * e1) + (double)xv.z * e2) + (double)xv.w * e3;
+      v[j] = __builtin_fma(x3, e3, __builtin_fma(x2, e2, __builtin_fma(x1, e1, __builtin_fma(x0, e0, v[j]))));
     }
 #pragma unroll
     for (int q = 0; q < P; ++q)
@@ -2612,8 +2630,8 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
     // streamer LDS: residual rows, [value tables of four blocks (2-bit codes)], the change list
     // being applied, member indices of two blocks (fused_config)
     double *eps_l = reinterpret_cast<double *>(smem);
-    float4 *s_lut = reinterpret_cast<float4 *>(eps_l + (int64_t)npass * SROWS);
-    double *s_pbo = reinterpret_cast<double *>(s_lut + (XF ? (d.lag + 3) * d.B : 0)), *s_pbn = s_pbo + (d.B + 16);
+    double *s_lut = eps_l + (int64_t)npass * SROWS;
+    double *s_pbo = s_lut + (XF ? (int64_t)(d.lag + 3) * d.B * 4 : 0), *s_pbn = s_pbo + (d.B + 16);
     int *s_pidx = reinterpret_cast<int *>(s_pbn + (d.B + 16));
     int *s_mem = s_pidx + (d.B + 16);  // 16-B aligned: B + 16 is a multiple of 4
     // (2-bit storage: s_mem holds the change positions instead); the apply's partial sums; then
@@ -2982,7 +3000,7 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   if ((size_t)nslot * d.B < solve_scratch_doubles(d.B, SWEEP_NT)) return false;
   // streamers: residual rows, [the value tables of two blocks], the change list (indices, old and
   // new betas), the member indices of two blocks in LDS
-  const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double) + (xf ? (size_t)d.B * 16 * (d.lag + 3) : 0) +
+  const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double) + (xf ? (size_t)d.B * 32 * (d.lag + 3) : 0) +
                            (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int)) + 2 * sizeof(int) * d.B +
                            (size_t)SWEEP_NW * SROWS * sizeof(double);
   const size_t code_bytes = xf ? (size_t)(d.lag + 2) * d.B * npass * 64 : 0;
