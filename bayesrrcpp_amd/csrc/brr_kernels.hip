@@ -1488,6 +1488,47 @@ __device__ __forceinline__ void chain_bayesr_resident(const Dev &d, int bs, doub
   }
 }
 
+// The chains as separate (not inlined) functions: inside the persistent k_sweep the solver's
+// chain shares the register allocation of every role (256 VGPRs and several hundred spilled SGPRs
+// whose reloads land in the chain's loop); called, a chain gets its own allocation (Horseshoe:
+// 220 -> 53 shader cycles per step in the fused kernel, the isolated microbenchmark's rate).  The LDS
+// operands travel as address-space-3 pointers so the callee still addresses them with ds_*
+// instructions (a generic pointer would make every read a flat access).
+#ifndef BRR_CHAIN_INLINE
+#define BRR_CHAIN_INLINE 0
+#endif
+// (the BayesR chain stays inline: called, its caller keeps ~400 VGPRs of live state in scratch
+// across the call and the streaming role of the same kernel slowed 2x at C3, measured)
+#ifndef BRR_BAYESR_CHAIN_CALL
+#define BRR_BAYESR_CHAIN_CALL 0
+#endif
+#define BRR_LDS __attribute__((address_space(3)))
+template <class T>
+__device__ __forceinline__ BRR_LDS T *to_lds(T *p) { return (BRR_LDS T *)p; }
+template <class T>
+__device__ __forceinline__ T *from_lds(BRR_LDS T *p) { return (T *)p; }
+
+template <int B>
+__device__ __attribute__((noinline)) void chain_hs_call(int bs, BRR_LDS const double *Lr0, BRR_LDS const double *Ldsel,
+                                                        BRR_LDS const double *Lsdz, BRR_LDS const double *Lbo,
+                                                        BRR_LDS double *Lbn, BRR_LDS const int *Lgi,
+                                                        BRR_LDS const double *coef) {
+  chain_hs_blocked<B>(bs, from_lds(Lr0), from_lds(Ldsel), from_lds(Lsdz), from_lds(Lbo), from_lds(Lbn), from_lds(Lgi),
+                      from_lds(coef));
+}
+
+template <int B>
+__device__ __attribute__((noinline)) void chain_bayesr_call(
+    const Dev &d, int bs, double sigmaE, BRR_LDS const double *Lr0, BRR_LDS const double *Llo, BRR_LDS const double *Lhi,
+    BRR_LDS const double *Ldsel, BRR_LDS const double *Lsdz, BRR_LDS const double *Lbo, BRR_LDS double *Lbn,
+    BRR_LDS const int *Lfl, BRR_LDS int *Lks, BRR_LDS const int *Lgi, BRR_LDS const double *La,
+    BRR_LDS const double *Lden, BRR_LDS const double *Lp, BRR_LDS const double *Lx2, BRR_LDS const double *Lz,
+    BRR_LDS const int *Lm, BRR_LDS const double *coef, bool prof) {
+  chain_bayesr_resident<B>(d, bs, sigmaE, from_lds(Lr0), from_lds(Llo), from_lds(Lhi), from_lds(Ldsel), from_lds(Lsdz),
+                           from_lds(Lbo), from_lds(Lbn), from_lds(Lfl), from_lds(Lks), from_lds(Lgi), from_lds(La),
+                           from_lds(Lden), from_lds(Lp), from_lds(Lx2), from_lds(Lz), from_lds(Lm), from_lds(coef), prof);
+}
+
 #ifndef BRR_EARLY_GRAM
 #define BRR_EARLY_GRAM 0
 #endif
@@ -1782,14 +1823,25 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     if (t < 64) {
       if constexpr (HS) {
         const uint64_t tq0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+#if BRR_CHAIN_INLINE
         chain_hs_blocked<B>(bs, Lr0, Ldsel, Lsdz, Lbo, Lbn, Lgi, slots);
+#else
+        chain_hs_call<B>(bs, to_lds(Lr0), to_lds(Ldsel), to_lds(Lsdz), to_lds(Lbo), to_lds(Lbn), to_lds(Lgi),
+                         to_lds(slots));
+#endif
         if (prof && lane == 0) {
           atomicAdd(&d.sc->prof[6], (unsigned long long)bs);
           atomicAdd(&d.sc->prof[12], (unsigned long long)(__builtin_amdgcn_s_memtime() - tq0));  // chain loop, shader clocks
         }
       } else {
+#if BRR_CHAIN_INLINE || !BRR_BAYESR_CHAIN_CALL
         chain_bayesr_resident<B>(d, bs, sigmaE, Lr0, Llo, Lhi, Ldsel, Lsdz, Lbo, Lbn, Lfl, Lks, Lgi, La, Lden, Lp,
                                  Lx2, Lz, Lm, slots, prof);
+#else
+        chain_bayesr_call<B>(d, bs, sigmaE, to_lds(Lr0), to_lds(Llo), to_lds(Lhi), to_lds(Ldsel), to_lds(Lsdz),
+                             to_lds(Lbo), to_lds(Lbn), to_lds(Lfl), to_lds(Lks), to_lds(Lgi), to_lds(La), to_lds(Lden),
+                             to_lds(Lp), to_lds(Lx2), to_lds(Lz), to_lds(Lm), to_lds(slots), prof);
+#endif
       }
     }
   } else if (HS && t < 64) {
