@@ -2215,6 +2215,9 @@ constexpr int FUSED_GROUP = FUSED_GROUP_N;
 // 2-bit storage: lsrc / ldst stage the next block's value tables (storage order, lcnt valid
 // entries, f32 in HBM -> 4 doubles per column in LDS) the same way; lutb = the value tables of
 // the block being applied (LDS, 4 doubles per column, by visit position).
+#ifndef BRR_APPLY_AB
+#define BRR_APPLY_AB 4
+#endif
 template <int XF>
 __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0, int64_t r1, int npass,
                                               double *eps_l, int *s_pidx, double *s_pbo, double *s_pbn,
@@ -2223,7 +2226,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
                                               int *s_ppos = nullptr, const float4 *lsrc = nullptr,
                                               double *ldst = nullptr, const double *lutb = nullptr, int lcnt = 0) {
 #pragma clang fp contract(off)
-  constexpr int AB = 4;  // columns per batch (two batches in flight: 8 KiB per wave, 32 VGPRs, as many as the
+  constexpr int AB = BRR_APPLY_AB;  // columns per batch (two batches in flight: 8 KiB per wave, 32 VGPRs, as many as the
                          // streaming ring leaves without spills)
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -2291,10 +2294,10 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
                 const double *lt = lutb + 4 * s_ppos[e + q];
                 const uint32_t b = r[q];
                 const double dd = s_pd[e + q];
-                a0 += lt[b & 3u] * dd;
-                a1 += lt[(b >> 2) & 3u] * dd;
-                a2 += lt[(b >> 4) & 3u] * dd;
-                a3 += lt[(b >> 6) & 3u] * dd;
+                a0 = __builtin_fma(lt[b & 3u], dd, a0);
+                a1 = __builtin_fma(lt[(b >> 2) & 3u], dd, a1);
+                a2 = __builtin_fma(lt[(b >> 4) & 3u], dd, a2);
+                a3 = __builtin_fma(lt[(b >> 6) & 3u], dd, a3);
               }
             }
           };
@@ -2323,11 +2326,11 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
 #pragma unroll
         for (int q = 0; q < AB; ++q) {
           if (e + q < e1) {
-            const double dd = s_pd[e + q];
-            a0 += (double)x[q].x * dd;
-            a1 += (double)x[q].y * dd;
-            a2 += (double)x[q].z * dd;
-            a3 += (double)x[q].w * dd;
+            const double dd = s_pd[e + q];  // (fused multiply-add, as the 2-bit path)
+            a0 = __builtin_fma((double)x[q].x, dd, a0);
+            a1 = __builtin_fma((double)x[q].y, dd, a1);
+            a2 = __builtin_fma((double)x[q].z, dd, a2);
+            a3 = __builtin_fma((double)x[q].w, dd, a3);
           }
         }
       };
