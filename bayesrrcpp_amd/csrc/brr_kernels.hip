@@ -2188,7 +2188,11 @@ constexpr int SWEEP_NW = SWEEP_NT / 64;
 #define STREAM_P 1    // items in flight ahead of the one being consumed (2+ spills at CW = 16)
 #endif
 #ifndef STREAM_P2
-#define STREAM_P2 6   // the same for 2-bit code tiles (one 16-byte load per item and lane)
+#define STREAM_P2 3   // the same for 2-bit code tiles (one 16-byte load per item and lane; P + 1 = 4
+                      // divides a 512-column block's items, so the static ring applies)
+#endif
+#ifndef BRR_STATIC_RING
+#define BRR_STATIC_RING 1  // stream_role: the ring unrolled by its length where it divides a block's items
 #endif
 // streaming workgroups (slab rows) per level-2 reduction group: 64 -> 4 reducer workgroups at C2
 // (16 / 32 / 64 measured 27.1 / 27.6 / 28.1 sweeps/s: fewer reducers, fewer slab2 rows for the
@@ -2488,11 +2492,13 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     if (q < total) issue(q, xq[q]);
   // diagnostics (prof): this workgroup's accumulated wait / apply / streaming time of the sweep
   uint64_t acc_wait = 0, acc_apply = 0, acc_stream = 0, t_mark = prof ? wall_clock64() : 0;
-  for (int it = 0; it < total; ++it) {
-    const int s = it / items, rem = it - s * items;
-    const int c = rem / npass, p = rem - c * npass;
-    const bool blk_end = rem == items - 1;
-    if (rem == 0 && s >= 1 && s <= LAG) {
+  // Item it: s = it / items (block), rem = position in the block; c = chunk, p = pass.
+  // boundary(s): block s's start (staging, or the apply of block s-1-LAG's changes);
+  // consume(it, xc): this item's dot contributions from its loaded data xc, and the wave reduction
+  // at a chunk's last pass; block_end(it, s, xn): the prefetch into xn issued after the partial-dot
+  // stores, their drain and the group-counter arrival.
+  auto boundary = [&](int s) __attribute__((always_inline)) {
+    if (s >= 1 && s <= LAG) {
       // a boundary without a change list to apply yet: stage block s+1's tables / indices
       if constexpr (XF) {
         if (s + 1 < nb) stage_lut(s + 1);  // (its buffer is not read before the barrier)
@@ -2502,7 +2508,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       }
       __syncthreads();
     }
-    if (rem == 0 && s >= LAG + 1) {
+    if (s >= LAG + 1) {
       // block boundary: apply block a = s-1-LAG's changes to the residual rows (lag 1: they
       // then hold every change before block s-1, which the solver corrects for through the
       // cross-Gram; lag 2: before block s-2, corrected for blocks s-2 and s-1)
@@ -2530,16 +2536,17 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
         t_mark = tn;
       }
     }
-    // prefetch P items ahead (across block boundaries) before consuming this one; at a block's
-    // last item the prefetch is issued after the partial-dot stores instead (see below)
-    if (!blk_end && it + P < total) issue(it + P, xq[P]);
+  };
+  auto consume = [&](int it, const Raw (&xc)[NR]) __attribute__((always_inline)) {
+    const int s = it / items, rem = it - s * items;
+    const int c = rem / npass, p = rem - c * npass;
     const double *e = eps_l + p * SROWS + 4 * lane;
     const double e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
     if constexpr (XF) {
       // code cache: block s's tile of group w CPW / 16 + c at this lane's row quad p 64 + lane
       if (s_codes)
         reinterpret_cast<uint4 *>(s_codes)[((s % NCC) * (B >> 4) + ((w * CPW + c * CW) >> 4)) * (npass * 64) + p * 64 +
-                                           lane] = xq[0][0];
+                                           lane] = xc[0];
     }
     // one fused multiply-add per value into the column's accumulator, rows in order (the same
     // operations on the same f64 values for both storages: the chains are identical)
@@ -2547,7 +2554,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     for (int j = 0; j < CW; ++j) {
       double x0, x1, x2, x3;
       if constexpr (XF) {
-        const uint32_t word = j < 4 ? xq[0][0].x : (j < 8 ? xq[0][0].y : (j < 12 ? xq[0][0].z : xq[0][0].w));
+        const uint32_t word = j < 4 ? xc[0].x : (j < 8 ? xc[0].y : (j < 12 ? xc[0].z : xc[0].w));
         const int sh = 8 * (j & 3);
         const double *lt = lut_of(s) + 4 * (w * CPW + c * CW + j);
         x0 = lt[__builtin_amdgcn_ubfe(word, sh, 2)];
@@ -2555,15 +2562,11 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
         x2 = lt[__builtin_amdgcn_ubfe(word, sh + 4, 2)];
         x3 = lt[__builtin_amdgcn_ubfe(word, sh + 6, 2)];
       } else {
-        const float4 xv = xq[0][j];
+        const float4 xv = xc[j];
         x0 = xv.x; x1 = xv.y; x2 = xv.z; x3 = xv.w;
       }
       v[j] = __builtin_fma(x3, e3, __builtin_fma(x2, e2, __builtin_fma(x1, e1, __builtin_fma(x0, e0, v[j]))));
     }
-#pragma unroll
-    for (int q = 0; q < P; ++q)
-#pragma unroll
-      for (int j = 0; j < NR; ++j) xq[q][j] = xq[q + 1][j];
     if (p == npass - 1) {
       // chunk done over this workgroup's rows: wave-reduce its CW columns
       double r;
@@ -2580,29 +2583,67 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       const int col = w * CPW + c * CW + lcol;
       if ((lane & (64 / CW - 1)) == 0) st_sc1(d.slab1 + (s % NPAR) * d.slab1_stride + (int64_t)g * B + col, r);
     }
-    if (blk_end) {
-      // block done.  The partial-dot stores were issued before the next item's loads, so
-      // waiting until only those loads are outstanding drains the stores (vmcnt counts in
-      // issue order) without draining the prefetch.
-      asm volatile("" ::: "memory");
-      if (it + P < total) issue(it + P, xq[P - 1]);
-      if (it + P < total) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P * NR) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // then one arrival on the group counter for the reducer workgroup (one per workgroup:
-      // per-wave arrivals measured 1.6x slower, contention on the group counters)
-      __syncthreads();
-      if (t == 0)
-        __hip_atomic_fetch_add(d.cnt1 + (s % NPAR) * d.NG + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t == 0) {
-        if (prof) {
-          tr_first(d, s, TR_ITEMS_FIRST);
-          tr_last(d, s, TR_ITEMS_LAST);
-          if (s == nb / 2) d.trace[(int64_t)nb * 16 + g] = wall_clock64();
-          const uint64_t tn = wall_clock64();
-          acc_stream += tn - t_mark;
-          t_mark = tn;
-        }
+  };
+  auto block_end = [&](int it, int s, Raw (&xn)[NR], bool clamp) __attribute__((always_inline)) {
+    // block done.  The partial-dot stores were issued before the next item's loads, so
+    // waiting until only those loads are outstanding drains the stores (vmcnt counts in
+    // issue order) without draining the prefetch.
+    asm volatile("" ::: "memory");
+    if (clamp || it + P < total) issue(clamp ? min(it + P, total - 1) : it + P, xn);
+    if (clamp || it + P < total) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P * NR) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // then one arrival on the group counter for the reducer workgroup (one per workgroup:
+    // per-wave arrivals measured 1.6x slower, contention on the group counters)
+    __syncthreads();
+    if (t == 0)
+      __hip_atomic_fetch_add(d.cnt1 + (s % NPAR) * d.NG + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == 0) {
+      if (prof) {
+        tr_first(d, s, TR_ITEMS_FIRST);
+        tr_last(d, s, TR_ITEMS_LAST);
+        if (s == nb / 2) d.trace[(int64_t)nb * 16 + g] = wall_clock64();
+        const uint64_t tn = wall_clock64();
+        acc_stream += tn - t_mark;
+        t_mark = tn;
       }
+    }
+  };
+  constexpr int R = P + 1;
+  if (BRR_STATIC_RING && items % R == 0) {
+    // static register ring: item it's data in xq[it % R], the loop unrolled by R so every slot
+    // index is a constant, and one load issued per item (clamped past the end), so the wait
+    // before a consume is for the oldest load only.  (A runtime ring shifts its elements, and
+    // the compiler then waits for every outstanding load before each consume:
+    // scripts/mb_decode.hip.)  R divides items: a block starts at u = 0 and ends at u = R - 1.
+    for (int it0 = 0; it0 < total; it0 += R) {
+      static_for<R>([&](auto uc) __attribute__((always_inline)) {
+        constexpr int u = decltype(uc)::value;
+        const int it = it0 + u;
+        const int s = it / items, rem = it - s * items;
+        if constexpr (u == 0)
+          if (rem == 0) boundary(s);
+        const bool blk_end = u == R - 1 && rem == items - 1;
+        if (!blk_end) issue(min(it + P, total - 1), xq[(u + P) % R]);
+        consume(it, xq[u]);
+        if constexpr (u == R - 1)
+          if (blk_end) block_end(it, s, xq[(u + P) % R], true);
+      });
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    for (int it = 0; it < total; ++it) {
+      const int s = it / items, rem = it - s * items;
+      const bool blk_end = rem == items - 1;
+      if (rem == 0) boundary(s);
+      // prefetch P items ahead (across block boundaries) before consuming this one; at a block's
+      // last item the prefetch is issued after the partial-dot stores instead (block_end)
+      if (!blk_end && it + P < total) issue(it + P, xq[P]);
+      consume(it, xq[0]);
+#pragma unroll
+      for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int j = 0; j < NR; ++j) xq[q][j] = xq[q + 1][j];
+      if (blk_end) block_end(it, s, xq[P - 1], false);
     }
   }
   if (prof && t == 0) {
