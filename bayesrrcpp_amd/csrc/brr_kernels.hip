@@ -375,8 +375,10 @@ __global__ __launch_bounds__(256) void k_gram(Dev d, const int *member, const in
   constexpr int QPC = KC / 4;  // row quads per column and chunk
   const float4 z4 = make_float4(0, 0, 0, 0);
   for (int64_t r0 = 0; r0 < ld; r0 += KC) {
+    static_assert((T * QPC) % 256 == 0, "whole loader rounds");
 #pragma unroll 4
-    for (int e = t; e < T * QPC; e += 256) {
+    for (int k = 0; k < T * QPC / 256; ++k) {
+      const int e = t + 256 * k;
       const int c = e / QPC, rq = (e - c * QPC) * 4;
       const int64_t ca = s_ca[c], cb = s_cb[c];
       float4 va, vb;
