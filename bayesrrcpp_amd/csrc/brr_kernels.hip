@@ -2245,11 +2245,31 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
   // this workgroup's rows) or in the HBM code tiles -- so a lane adds only its quad
   int64_t *s_cb = reinterpret_cast<int64_t *>(s_pbn);
   if (t < 64) {
-    const int np = ld_sc1_int(d.pend_n + slot);
-    const int nr = ld_sc1_int(d.pend_n + NSLOT + slot);  // entries before the neutral padding
     const int *pidx = d.pend_idx + slot * d.pend_stride;
     const double *pbo = d.pend_bo + slot * d.pend_stride, *pbn = d.pend_bn + slot * d.pend_stride;
-    for (int e = lane; e < np; e += 64) {
+    // one round trip for the counts and every lane's first entry together (the list arrays hold
+    // at least B >= 64 entries, so entry `lane` is always addressable; entries past np are unused)
+    const int np = ld_sc1_int(d.pend_n + slot);
+    const int nr = ld_sc1_int(d.pend_n + NSLOT + slot);  // entries before the neutral padding
+    int col0 = ld_sc1_int(pidx + lane);
+    int gi0 = XF ? ld_sc1_int(d.pend_gi + slot * d.pend_stride + lane) : 0;
+    const double pd0 = ld_sc1(pbo + lane) - ld_sc1(pbn + lane);
+    {
+      // neutral padding entries (e >= nr: b_old = b_new = 0) take the last real entry's column: a
+      // cache hit instead of column 0 from HBM, and no branch in the batched loads
+      const int src = lane < nr ? lane : max(nr - 1, 0);
+      col0 = __shfl(col0, src);
+      if (XF) gi0 = __shfl(gi0, src);
+      if (lane < np) {
+        s_pidx[lane] = col0;
+        if (XF) {
+          s_ppos[lane] = gi0;
+          s_cb[lane] = ccode ? (int64_t)(gi0 >> 4) * (npass * 64 * 16) + (gi0 & 15) : code_off(col0, 0, d.B, d.ldc);
+        }
+        s_pd[lane] = pd0;
+      }
+    }
+    for (int e = lane + 64; e < np; e += 64) {
       // neutral padding entries (b_old = b_new = 0) load the last real column again: a cache
       // hit instead of column 0 from HBM, and no branch in the batched loads
       const int es = e < nr ? e : max(nr - 1, 0);
