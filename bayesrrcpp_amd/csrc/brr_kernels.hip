@@ -2230,8 +2230,13 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
                                               int *s_np, double *s_part, const int *msrc = nullptr,
                                               int *mdst = nullptr, const uint8_t *ccode = nullptr,
                                               int *s_ppos = nullptr, const float4 *lsrc = nullptr,
-                                              double *ldst = nullptr, const double *lutb = nullptr, int lcnt = 0) {
+                                              double *ldst = nullptr, const double *lutb = nullptr, int lcnt = 0,
+                                              uint64_t *ptime = nullptr) {
 #pragma clang fp contract(off)
+  // diagnostics (ptime, thread 0): [0] += list staging incl. its barrier, [1] += this wave's
+  // products, [2] += the wait for the other waves' parts, [3] += the staging stores and the last
+  // barrier (bench.py --profile-solve: wg_apply_{list,products,partbar,stage}_ms_pct)
+  const uint64_t tq0 = ptime ? wall_clock64() : 0;
   constexpr int AB = BRR_APPLY_AB;  // columns per batch (two batches in flight: 8 KiB per wave, 32 VGPRs, as many as the
                          // streaming ring leaves without spills)
   const int t = threadIdx.x, lane = t & 63;
@@ -2286,6 +2291,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
   }
   __syncthreads();
   const int np = __builtin_amdgcn_readfirstlane(s_np[0]);
+  const uint64_t tq1 = ptime ? wall_clock64() : 0;
   const int G = npass >= SWEEP_NW ? 1 : SWEEP_NW / npass;  // parts of the list
   const int ldp = npass * SROWS;                          // doubles per part in s_part
   if (np > 0) {
@@ -2393,6 +2399,8 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
         pp[3] = a3;
       }
     }
+    const uint64_t tq2 = ptime ? wall_clock64() : 0;
+    if (ptime) { ptime[0] += tq1 - tq0; ptime[1] += tq2 - tq1; }
     if (G > 1) {
       // parts without a pass (G npass < 8 waves, or an empty part) hold nothing: zero them first
       for (int i = t; i < G * ldp; i += SWEEP_NT) {
@@ -2400,6 +2408,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
         if (np * part / G == np * (part + 1) / G) s_part[i] = 0.0;
       }
       __syncthreads();
+      if (ptime) ptime[2] += wall_clock64() - tq2;
       for (int i = t; i < ldp; i += SWEEP_NT) {
         if (r0 + i < r1) {
           double acc = s_part[i];
@@ -2409,12 +2418,14 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
       }
     }
   }
+  const uint64_t tq4 = ptime ? wall_clock64() : 0;
   if (mcopy) mdst[t] = mval;
   if (lcopy) {
     double *l = ldst + 4 * t;
     l[0] = lval.x; l[1] = lval.y; l[2] = lval.z; l[3] = lval.w;
   }
   __syncthreads();
+  if (ptime) ptime[3] += wall_clock64() - tq4;
 }
 
 // XF = 1: 2-bit genotype codes in tiles (brr_device.hpp).  A block is streamed in STORAGE order:
@@ -2514,6 +2525,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     if (q < total) issue(q, xq[q]);
   // diagnostics (prof): this workgroup's accumulated wait / apply / streaming time of the sweep
   uint64_t acc_wait = 0, acc_apply = 0, acc_stream = 0, t_mark = prof ? wall_clock64() : 0;
+  uint64_t acc_sub[4] = {0, 0, 0, 0};  // apply: list staging, products, part barrier, staging stores (ptime)
   // Item it: s = it / items (block), rem = position in the block; c = chunk, p = pass.
   // boundary(s): block s's start (staging, or the apply of block s-1-LAG's changes);
   // consume(it, xc): this item's dot contributions from its loaded data xc, and the wave reduction
@@ -2549,7 +2561,8 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
                         (!XF && s + 1 < nb) ? d.member + (int64_t)(s + 1) * B : nullptr, s_mem + ((s + 1) & 1) * B,
                         cache_of(a), s_mem,
                         (XF && s + 1 < nb) ? reinterpret_cast<const float4 *>(d.xlut) + (int64_t)d.gblk[s + 1] * B : nullptr,
-                        lut_of(s + 1), lut_of(a), (XF && s + 1 < nb) ? d.bsz[s + 1] : 0);
+                        lut_of(s + 1), lut_of(a), (XF && s + 1 < nb) ? d.bsz[s + 1] : 0,
+                        (prof && t == 0) ? acc_sub : nullptr);
       if (prof && t == 0) {
         tr_last(d, s, TR_APPLY_LAST);
         if (s == nb / 2) d.trace[(int64_t)nb * 16 + 1024 + g] = wall_clock64();  // per-workgroup probe
@@ -2673,6 +2686,10 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     acc[g] = acc_wait;
     acc[1024 + g] = acc_apply;
     acc[2048 + g] = acc_stream;
+    acc[3072 + g] = acc_sub[0];
+    acc[4096 + g] = acc_sub[1];
+    acc[5120 + g] = acc_sub[2];
+    acc[6144 + g] = acc_sub[3];
   }
   // end of sweep: the last LAG + 1 blocks' changes, then the residual rows back to HBM
   if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + nb, d.sync, 4);

@@ -866,7 +866,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   rc |= s->alloc(&d.pend_bo, NSLOT * d.pend_stride);
   rc |= s->alloc(&d.pend_bn, NSLOT * d.pend_stride);
   rc |= s->alloc(&d.pend_n, 2 * NSLOT);  // [NSLOT] padded list lengths, [NSLOT] entries before the padding
-  rc |= s->alloc(&d.trace, (int64_t)s->nb * 16 + 5120);  // + per-workgroup probes and totals
+  rc |= s->alloc(&d.trace, (int64_t)s->nb * 16 + 9216);  // + per-workgroup probes and totals
   d.nbB = (int64_t)s->nb * B;
   rc |= s->alloc(&d.mc, d.nbB * (3 + 2 * std::max(K, 1)));
   rc |= s->alloc(&d.rslab, 2 * RGrows);
@@ -1477,7 +1477,7 @@ int brr_session_set_scalar(brr_session *s, int32_t which, double v) {
     case 102:  // diagnostics: k_solve phase timers on/off (resets the totals)
       sc.prof_on = v != 0.0;
       for (auto &x : sc.prof) x = 0;
-      HIPCHK(hipMemsetAsync(s->d.trace, 0, sizeof(unsigned long long) * (16 * (size_t)s->nb + 5120), s->st));
+      HIPCHK(hipMemsetAsync(s->d.trace, 0, sizeof(unsigned long long) * (16 * (size_t)s->nb + 9216), s->st));
       break;
     default: set_error("scalar %d not settable", which); return -1;
   }
@@ -1496,7 +1496,7 @@ int64_t brr_session_get_vector(brr_session *s, int32_t which, double *out) {
     case BRR_PI: case BRR_VCOUNT: n = (int64_t)s->G * s->K; break;
     case BRR_ALPHA: n = s->F; break;
     case 200: n = s->M; break;  // diagnostics: column sums of the device X (not in brr.h)
-    case 201: n = (int64_t)s->nb * 16 + 5120; break;  // diagnostics: per-block event trace (brr_kernels.hip TR_*)
+    case 201: n = (int64_t)s->nb * 16 + 9216; break;  // diagnostics: per-block event trace (brr_kernels.hip TR_*)
     default: set_error("unknown vector %d", which); return -1;
   }
   if (!out) return n;

@@ -53,10 +53,10 @@ def block_events(raw, lag=1):
     publication of block s-1-lag's changes, which is what streaming block s waits for."""
     import numpy as np
     raw = np.asarray(raw, dtype=np.float64)
-    nbk = (raw.size - 5120) // 16
+    nbk = (raw.size - 9216) // 16
     tr = raw[:nbk * 16].reshape(-1, 16)
     probe = raw[nbk * 16:nbk * 16 + 2048].reshape(2, 1024)
-    acc = raw[nbk * 16 + 2048:].reshape(3, 1024)  # per streaming workgroup: wait, apply, stream
+    acc = raw[nbk * 16 + 2048:].reshape(7, 1024)  # per streaming workgroup: wait, apply, stream; apply: list, products, part barrier, staging stores
     u64 = float(2 ** 64)
     first = lambda c: u64 - 1 - tr[:, c]  # noqa: E731  (stored as ~t)
     nb = tr.shape[0]
@@ -98,6 +98,10 @@ def block_events(raw, lag=1):
         out["wg_wait_ms_pct"] = ms(np.percentile(acc[0][w], [0, 10, 50, 90, 100]))
         out["wg_apply_ms_pct"] = ms(np.percentile(acc[1][w], [0, 10, 50, 90, 100]))
         out["wg_stream_ms_pct"] = ms(np.percentile(acc[2][w], [0, 10, 50, 90, 100]))
+        out["wg_apply_list_ms_pct"] = ms(np.percentile(acc[3][w], [0, 10, 50, 90, 100]))
+        out["wg_apply_products_ms_pct"] = ms(np.percentile(acc[4][w], [0, 10, 50, 90, 100]))
+        out["wg_apply_partbar_ms_pct"] = ms(np.percentile(acc[5][w], [0, 10, 50, 90, 100]))
+        out["wg_apply_stage_ms_pct"] = ms(np.percentile(acc[6][w], [0, 10, 50, 90, 100]))
         out["wg_busy_by_xcd_ms"] = ms([np.mean(busy[w][(w + 1) % 8 == x]) for x in range(8)])
         out["wg_slowest"] = [int(x) for x in w[np.argsort(busy[w])[-8:]]]
     return out
