@@ -11,12 +11,14 @@
 #define _POSIX_C_SOURCE 200809L
 #include "brr_oracle.h"
 
+#include <float.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #define ORC_MAXK 16
+#define ORC_LN2 0.693147180559945309417232121458
 #define ORC_GAMMA_MAX_ATTEMPTS 64
 
 /* ------------------------------------------------------------------------- */
@@ -51,10 +53,282 @@ double orc_u53(uint32_t hi, uint32_t lo) {
   return ((double)x + 0.5) * 0x1p-53;
 }
 
+/* ------------------------------------------------------------------------- */
+/* r_compat backend: R's default generators, restated from R's published
+ * nmath / RNG.c algorithms (R itself is not in this image): Mersenne-Twister unif_rand with
+ * set.seed's scrambling, Inversion norm_rand (qnorm5, Wichura AS241), exp_rand (Ahrens &
+ * Dieter 1972 SA), rgamma (Ahrens & Dieter 1982 GD for a >= 1, 1974 GS for a < 1) and
+ * rbeta(1,1) (Cheng 1978 BC, the only beta the reference draws: src/distributions.cpp:58).
+ * The draws are taken from ONE sequential stream in the reference's call order (the
+ * samplers below call them in that order), so given R's set.seed value the chain would be
+ * the reference's own.  Pinned: unif_rand / norm_rand against R's documented outputs
+ * (tests/test_oracle.py, set.seed(42) runif, set.seed(1) / set.seed(123) rnorm);
+ * exp_rand / rgamma / rbeta: parity unpinned (no R here), checked by moments only. */
+#define R_MT_N 624
+#define R_MT_M 397
+struct orc_rstream {
+  uint32_t mt[R_MT_N];
+  int mti;
+  double aa, aaa, s, s2, d, q0, b, si, c; /* rgamma's saved constants (rgamma.c statics) */
+};
+
+/* set.seed(seed) with kind = "Mersenne-Twister" (RNG.c Randomize / RNG_Init / FixupSeeds):
+ * 50 initial LCG scrambles, then 625 LCG outputs: dummy[0] (mti, forced to 624) and mt[] */
+orc_rstream *orc_rstream_create(uint32_t seed) {
+  orc_rstream *r = (orc_rstream *)calloc(1, sizeof(orc_rstream));
+  for (int j = 0; j < 50; ++j) seed = 69069u * seed + 1u;
+  seed = 69069u * seed + 1u; /* i_seed[0] = dummy[0] (mti), reset to N by FixupSeeds */
+  for (int j = 0; j < R_MT_N; ++j) {
+    seed = 69069u * seed + 1u;
+    r->mt[j] = seed;
+  }
+  r->mti = R_MT_N;
+  r->aa = r->aaa = 0.0;
+  return r;
+}
+void orc_rstream_destroy(orc_rstream *r) { free(r); }
+
+static double r_mt_genrand(orc_rstream *r) {
+  static const uint32_t mag01[2] = {0x0u, 0x9908b0dfu};
+  uint32_t y;
+  if (r->mti >= R_MT_N) {
+    int kk;
+    for (kk = 0; kk < R_MT_N - R_MT_M; ++kk) {
+      y = (r->mt[kk] & 0x80000000u) | (r->mt[kk + 1] & 0x7fffffffu);
+      r->mt[kk] = r->mt[kk + R_MT_M] ^ (y >> 1) ^ mag01[y & 1u];
+    }
+    for (; kk < R_MT_N - 1; ++kk) {
+      y = (r->mt[kk] & 0x80000000u) | (r->mt[kk + 1] & 0x7fffffffu);
+      r->mt[kk] = r->mt[kk + (R_MT_M - R_MT_N)] ^ (y >> 1) ^ mag01[y & 1u];
+    }
+    y = (r->mt[R_MT_N - 1] & 0x80000000u) | (r->mt[0] & 0x7fffffffu);
+    r->mt[R_MT_N - 1] = r->mt[R_MT_M - 1] ^ (y >> 1) ^ mag01[y & 1u];
+    r->mti = 0;
+  }
+  y = r->mt[r->mti++];
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return (double)y * 2.3283064365386963e-10; /* [0,1) */
+}
+
+/* unif_rand(): MT_genrand through fixup() (strictly inside (0,1)) */
+double orc_r_unif(orc_rstream *r) {
+  const double i2_32m1 = 2.328306437080797e-10; /* 1/(2^32 - 1) */
+  double v = r_mt_genrand(r);
+  if (v <= 0.0) return 0.5 * i2_32m1;
+  if (1.0 - v <= 0.0) return 1.0 - 0.5 * i2_32m1;
+  return v;
+}
+
+/* qnorm(p, 0, 1, lower = TRUE, log = FALSE): Wichura (1988) AS241 PPND16 */
+static double r_qnorm(double p) {
+  const double q = p - 0.5;
+  double r, val;
+  if (fabs(q) <= 0.425) {
+    r = 0.180625 - q * q;
+    return q * (((((((r * 2509.0809287301226727 + 33430.575583588128105) * r + 67265.770927008700853) * r +
+                    45921.953931549871457) * r + 13731.693765509461125) * r + 1971.5909503065514427) * r +
+                 133.14166789178437745) * r + 3.387132872796366608) /
+           (((((((r * 5226.495278852545925 + 28729.085735721942674) * r + 39307.89580009271061) * r +
+                21213.794301586595867) * r + 5394.1960214247511077) * r + 687.1870074920579083) * r +
+             42.313330701600911252) * r + 1.0);
+  }
+  r = q < 0 ? p : 1.0 - p;
+  r = sqrt(-log(r));
+  if (r <= 5.0) {
+    r += -1.6;
+    val = (((((((r * 7.7454501427834140764e-4 + 0.0227238449892691845833) * r + 0.24178072517745061177) * r +
+               1.27045825245236838258) * r + 3.64784832476320460504) * r + 5.7694972214606914055) * r +
+            4.6303378461565452959) * r + 1.42343711074968357734) /
+          (((((((r * 1.05075007164441684324e-9 + 5.475938084995344946e-4) * r + 0.0151986665636164571966) * r +
+               0.14810397642748007459) * r + 0.68976733498510000455) * r + 1.6763848301838038494) * r +
+            2.05319162663775882187) * r + 1.0);
+  } else {
+    r += -5.0;
+    val = (((((((r * 2.01033439929228813265e-7 + 2.71155556874348757815e-5) * r + 0.0012426609473880784386) * r +
+               0.026532189526576123093) * r + 0.29656057182850489123) * r + 1.7848265399172913358) * r +
+            5.4637849111641143699) * r + 6.6579046435011037772) /
+          (((((((r * 2.04426310338993978564e-15 + 1.4215117583164458887e-7) * r + 1.8463183175100546818e-5) * r +
+               7.868691311456132591e-4) * r + 0.0148753612908506148525) * r + 0.13692988092273580531) * r +
+            0.59983220655588793769) * r + 1.0);
+  }
+  return q < 0.0 ? -val : val;
+}
+
+/* norm_rand() with normal.kind = "Inversion": two uniforms for 2^27-fold resolution */
+double orc_r_norm(orc_rstream *r) {
+  const double BIG = 134217728.0; /* 2^27 */
+  double u = orc_r_unif(r);
+  u = (int)(BIG * u) + orc_r_unif(r);
+  return r_qnorm(u / BIG);
+}
+
+/* exp_rand(): Ahrens & Dieter (1972) algorithm SA; q[k] = sum_{i=1..k+1} ln2^i / i! */
+double orc_r_exp(orc_rstream *r) {
+  static double q[16];
+  static int qinit = 0;
+  if (!qinit) {
+    double term = 1.0, s = 0.0;
+    for (int k = 0; k < 16; ++k) {
+      term *= ORC_LN2 / (double)(k + 1);
+      s += term;
+      q[k] = s;
+    }
+    q[15] = 1.0;
+    qinit = 1;
+  }
+  double a = 0.0;
+  double u = orc_r_unif(r);
+  while (u <= 0.0 || u >= 1.0) u = orc_r_unif(r);
+  for (;;) {
+    u += u;
+    if (u > 1.0) break;
+    a += q[0];
+  }
+  u -= 1.0;
+  if (u <= q[0]) return a + u;
+  int i = 0;
+  double ustar = orc_r_unif(r), umin = ustar;
+  do {
+    ustar = orc_r_unif(r);
+    if (umin > ustar) umin = ustar;
+    i++;
+  } while (u > q[i]);
+  return a + umin * q[0];
+}
+
+/* rgamma(a, scale = 1) (nmath/rgamma.c) */
+double orc_r_gamma(orc_rstream *r, double a) {
+  const double sqrt32 = 5.656854, exp_m1 = 0.36787944117144233;
+  const double q1 = 0.04166669, q2 = 0.02083148, q3 = 0.00801191, q4 = 0.00144121, q5 = -7.388e-5,
+               q6 = 2.4511e-4, q7 = 2.424e-4;
+  const double a1 = 0.3333333, a2 = -0.250003, a3 = 0.2000062, a4 = -0.1662921, a5 = 0.1423657,
+               a6 = -0.1367177, a7 = 0.1233795;
+  double e, p, q, t, u, v, w, x, ret_val;
+  if (!(a > 0.0)) return 0.0;
+  if (a < 1.0) { /* GS */
+    e = 1.0 + exp_m1 * a;
+    for (;;) {
+      p = e * orc_r_unif(r);
+      if (p >= 1.0) {
+        x = -log((e - p) / a);
+        if (orc_r_exp(r) >= (1.0 - a) * log(x)) break;
+      } else {
+        x = exp(log(p) / a);
+        if (orc_r_exp(r) >= x) break;
+      }
+    }
+    return x;
+  }
+  if (a != r->aa) {
+    r->aa = a;
+    r->s2 = a - 0.5;
+    r->s = sqrt(r->s2);
+    r->d = sqrt32 - r->s * 12.0;
+  }
+  const double s = r->s, s2 = r->s2, d = r->d;
+  t = orc_r_norm(r);
+  x = s + 0.5 * t;
+  ret_val = x * x;
+  if (t >= 0.0) return ret_val;
+  u = orc_r_unif(r);
+  if (d * u <= t * t * t) return ret_val;
+  if (a != r->aaa) {
+    r->aaa = a;
+    const double rr = 1.0 / a;
+    r->q0 = ((((((q7 * rr + q6) * rr + q5) * rr + q4) * rr + q3) * rr + q2) * rr + q1) * rr;
+    if (a <= 3.686) {
+      r->b = 0.463 + s + 0.178 * s2;
+      r->si = 1.235;
+      r->c = 0.195 / s - 0.079 + 0.16 * s;
+    } else if (a <= 13.022) {
+      r->b = 1.654 + 0.0076 * s2;
+      r->si = 1.68 / s + 0.275;
+      r->c = 0.062 / s + 0.024;
+    } else {
+      r->b = 1.77;
+      r->si = 0.75;
+      r->c = 0.1515 / s;
+    }
+  }
+  const double q0 = r->q0, b = r->b, si = r->si, c = r->c;
+  if (x > 0.0) {
+    v = t / (s + s);
+    if (fabs(v) <= 0.25)
+      q = q0 + 0.5 * t * t * ((((((a7 * v + a6) * v + a5) * v + a4) * v + a3) * v + a2) * v + a1) * v;
+    else
+      q = q0 - s * t + 0.25 * t * t + (s2 + s2) * log(1.0 + v);
+    if (log(1.0 - u) <= q) return ret_val;
+  }
+  for (;;) {
+    e = orc_r_exp(r);
+    u = orc_r_unif(r);
+    u = u + u - 1.0;
+    t = u < 0.0 ? b - si * e : b + si * e;
+    if (t >= -0.71874483771719) {
+      v = t / (s + s);
+      if (fabs(v) <= 0.25)
+        q = q0 + 0.5 * t * t * ((((((a7 * v + a6) * v + a5) * v + a4) * v + a3) * v + a2) * v + a1) * v;
+      else
+        q = q0 - s * t + 0.25 * t * t + (s2 + s2) * log(1.0 + v);
+      if (q > 0.0) {
+        w = expm1(q);
+        if (c * fabs(u) <= w * exp(e - 0.5 * t * t)) break;
+      }
+    }
+  }
+  x = s + 0.5 * t;
+  return x * x;
+}
+
+/* rbeta(1, 1): Cheng (1978) algorithm BC with a = b = 1 (beta = 1, delta = 1, k1 = 0.25,
+ * k2 = 1, alpha = 2), returning a / (a + w) as rbeta.c does when aa == max(aa, bb) */
+double orc_r_beta11(orc_rstream *r) {
+  const double a = 1.0, alpha = 2.0, beta = 1.0, k1 = 0.25, k2 = 1.0;
+  const double expmax = DBL_MAX_EXP * ORC_LN2;
+  double u1, u2, v = 0.0, w = 0.0, y, z;
+  for (;;) {
+    u1 = orc_r_unif(r);
+    u2 = orc_r_unif(r);
+    if (u1 < 0.5) {
+      y = u1 * u2;
+      z = u1 * y;
+      if (0.25 * u2 + z - y >= k1) continue;
+    } else {
+      z = u1 * u1 * u2;
+      if (z <= 0.25) {
+        v = beta * log(u1 / (1.0 - u1));
+        w = v <= expmax ? a * exp(v) : DBL_MAX;
+        if (!isfinite(w)) w = DBL_MAX;
+        break;
+      }
+      if (z >= k2) continue;
+    }
+    v = beta * log(u1 / (1.0 - u1));
+    w = v <= expmax ? a * exp(v) : DBL_MAX;
+    if (!isfinite(w)) w = DBL_MAX;
+    if (alpha * (log(alpha / (a + w)) + v) - 1.3862944 >= log(z)) break;
+  }
+  return a / (a + w);
+}
+
+/* the stream of the orc being driven (set by the public entry points): NULL = Philox */
+static __thread orc_rstream *g_rs = NULL;
+
 double orc_uniform(uint64_t seed, uint32_t tag, uint32_t entity, uint32_t it, uint32_t slot) {
+  if (g_rs) return orc_r_unif(g_rs); /* R::runif(0, 1) = unif_rand() */
   uint32_t w[4];
   philox_draw(seed, slot, tag, entity, it, w);
   return orc_u53(w[0], w[1]);
+}
+
+/* beta_rng(1,1) call sites (src/distributions.cpp:58): a uniform under Philox, R::rbeta(1,1)
+ * under r_compat */
+static double orc_beta11(uint64_t seed, uint32_t tag, uint32_t entity, uint32_t it, uint32_t slot) {
+  if (g_rs) return orc_r_beta11(g_rs);
+  return orc_uniform(seed, tag, entity, it, slot);
 }
 
 static double box_muller(const uint32_t w[4]) {
@@ -64,6 +338,7 @@ static double box_muller(const uint32_t w[4]) {
 }
 
 double orc_normal(uint64_t seed, uint32_t tag, uint32_t entity, uint32_t it, uint32_t slot) {
+  if (g_rs) return orc_r_norm(g_rs); /* R::rnorm(mean, sd) = mean + sd * norm_rand() */
   uint32_t w[4];
   philox_draw(seed, slot, tag, entity, it, w);
   return box_muller(w);
@@ -74,6 +349,7 @@ double orc_normal(uint64_t seed, uint32_t tag, uint32_t entity, uint32_t it, uin
  * slot 0xFFFFFFFF.  Replaces R::rgamma (src/distributions.cpp:17,22,25,31). */
 double orc_gamma(uint64_t seed, double shape, uint32_t tag, uint32_t entity, uint32_t it) {
   if (!(shape > 0.0)) return 0.0;
+  if (g_rs) return orc_r_gamma(g_rs, shape); /* R::rgamma(shape, 1); callers apply the scale */
   double boost = 1.0;
   double a = shape;
   if (a < 1.0) {
@@ -226,6 +502,7 @@ struct orc {
   glibc_rand grand;
   double *stats;      /* [sum b^2, sum b^2/lambda, betaAcum[G], v[G*K]] used by the epilogue */
   double *deps;       /* shard_only: this shard's eps - eps_start */
+  orc_rstream *rs;    /* r_compat stream (orc_set_rng_r), NULL = Philox */
 };
 
 static double *dalloc(int64_t n) { return (double *)calloc((size_t)(n > 0 ? n : 1), sizeof(double)); }
@@ -275,6 +552,7 @@ void orc_destroy(orc *o) {
   free(o->comp); free(o->xsq); free(o->lambda); free(o->hsv); free(o->sigmaGG); free(o->pi);
   free(o->v); free(o->betaAcum); free(o->alpha); free(o->order); free(o->forder);
   free(o->stats); free(o->deps);
+  orc_rstream_destroy(o->rs);
   free(o);
 }
 
@@ -294,7 +572,21 @@ static double sqnorm(const double *x, int64_t n) {
   return s;
 }
 
+int orc_set_rng_r(orc *o, int on, uint32_t r_seed) {
+  orc_rstream_destroy(o->rs);
+  o->rs = on ? orc_rstream_create(r_seed) : NULL;
+  return 0;
+}
+
+static int orc_init_body(orc *o);
 int orc_init(orc *o) {
+  g_rs = o->rs;
+  const int rc = orc_init_body(o);
+  g_rs = NULL;
+  return rc;
+}
+
+static int orc_init_body(orc *o) {
   const int64_t N = o->N, P = o->P;
   const int K = o->K, G = o->G;
   const uint32_t IT = ORC_INIT_IT;
@@ -314,10 +606,10 @@ int orc_init(orc *o) {
       for (int64_t m = 0; m < P; ++m) { o->beta[m] = 0.0; o->comp[m] = 0.0; }
       o->mu = 0.0;
       if (o->c.model == ORC_V2) {
-        o->sigmaGG[0] = orc_uniform(o->seed, ORC_T_INIT, 0, IT, 0); /* beta_rng(1,1) :162 */
+        o->sigmaGG[0] = orc_beta11(o->seed, ORC_T_INIT, 0, IT, 0); /* beta_rng(1,1) :162 */
       } else {
         for (int g = 0; g < G; ++g) /* :194-195 */
-          o->sigmaGG[g] = orc_uniform(o->seed, ORC_T_INIT, (uint32_t)g, IT, 0);
+          o->sigmaGG[g] = orc_beta11(o->seed, ORC_T_INIT, (uint32_t)g, IT, 0);
         o->sigmaF = orc_uniform(o->seed, ORC_T_INIT, 0x10000000u, IT, 0); /* R::runif :197 */
         for (int f = 0; f < o->F; ++f) o->alpha[f] = 0.0;
       }
@@ -346,7 +638,12 @@ int orc_init(orc *o) {
     case ORC_HORSESHOE: {
       /* HorseshoeR.cpp:168-195.  The 2*M discarded init draws (:176,:179) and the
        * overwritten tau=rbeta(1,1) (:171) consume R's stream only; counter-based draws
-       * make them no-ops, so they are skipped. */
+       * make them no-ops, so they are skipped; a sequential R stream consumes them. */
+      if (g_rs) {
+        (void)orc_r_beta11(g_rs);                                                /* :171 */
+        for (int64_t m = 0; m < P; ++m) (void)orc_r_gamma(g_rs, 0.5);            /* :176 */
+        for (int64_t m = 0; m < P; ++m) (void)orc_r_gamma(g_rs, 0.5 * o->c.vL);  /* :179 */
+      }
       for (int64_t m = 0; m < P; ++m) { o->beta[m] = 0.0; o->hsv[m] = 1.0; o->lambda[m] = 1.0; }
       o->mu = 0.0;
       o->c2 = o->c.c2;
@@ -427,7 +724,9 @@ static void bayesr_marker(orc *o, int64_t m, double *eps) {
     logL[k] = logL[k] - 0.5 * log(((sigmaG / sigmaE) * o->xsq[m]) * cVa[k] + 1.0) +
               (0.5 * (muk[k] * num)) / sigmaE;
   const uint32_t mg = (uint32_t)m;
-  const double p = orc_uniform(o->seed, ORC_T_MARKER, mg, (uint32_t)o->it, 0); /* :213 / :266 */
+  /* V2 :213 / restart :217 beta_rng(1,1); Groups :266 R::runif(0,1) */
+  const double p = o->c.model == ORC_GROUPS ? orc_uniform(o->seed, ORC_T_MARKER, mg, (uint32_t)o->it, 0)
+                                            : orc_beta11(o->seed, ORC_T_MARKER, mg, (uint32_t)o->it, 0);
   double acum;
   int guard = 0;
   for (int i = 1; i < K; ++i) guard |= fabs(logL[i] - logL[0]) > 700.0;     /* :216 */
@@ -676,7 +975,9 @@ static void hs_epilogue(orc *o) {
 
 int orc_sweep_local(orc *o) {
   if (o->c.shard_only < 0) return -1;
+  g_rs = o->rs;
   if (o->c.model == ORC_HORSESHOE) sweep_horseshoe(o); else sweep_bayesr(o);
+  g_rs = NULL;
   return 0;
 }
 
@@ -695,16 +996,20 @@ int orc_exchange_set(orc *o, const double *deps_sum, const double *stats_sum) {
 }
 
 int orc_sweep_finish(orc *o) {
+  g_rs = o->rs;
   if (o->c.model == ORC_HORSESHOE) hs_epilogue(o); else bayesr_epilogue(o);
+  g_rs = NULL;
   o->it++;
   return 0;
 }
 
 int orc_sweep(orc *o, int n) {
+  g_rs = o->rs;
   for (int r = 0; r < n; ++r) {
     if (o->c.model == ORC_HORSESHOE) sweep_horseshoe(o); else sweep_bayesr(o);
     o->it++;
   }
+  g_rs = NULL;
   return 0;
 }
 

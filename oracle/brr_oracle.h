@@ -111,6 +111,20 @@ int orc_set_vector(orc *o, int which, const double *in);
 int orc_set_scalar(orc *o, int which, double v);
 
 /* ---- RNG primitives (exported for KAT / cross-implementation tests) ---- */
+/* r_compat RNG backend: R's Mersenne-Twister / Inversion / rgamma /
+ * rbeta(1,1) as one sequential stream seeded like set.seed(r_seed).  orc_set_rng_r(o, 1, s)
+ * before orc_init makes every draw of that chain come from it, in the reference's call order;
+ * (o, 0, 0) returns to Philox.  See brr_oracle.c for what is pinned. */
+typedef struct orc_rstream orc_rstream;
+int orc_set_rng_r(orc *o, int on, uint32_t r_seed);
+orc_rstream *orc_rstream_create(uint32_t r_seed);
+void orc_rstream_destroy(orc_rstream *r);
+double orc_r_unif(orc_rstream *r);
+double orc_r_norm(orc_rstream *r);
+double orc_r_exp(orc_rstream *r);
+double orc_r_gamma(orc_rstream *r, double shape);
+double orc_r_beta11(orc_rstream *r);
+
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 double orc_u53(uint32_t hi, uint32_t lo);
 double orc_uniform(uint64_t seed, uint32_t tag, uint32_t entity, uint32_t it, uint32_t slot);

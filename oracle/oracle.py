@@ -98,6 +98,15 @@ def lib():
         L.orc_stats_size.argtypes = [C.c_void_p]
         L.orc_exchange_get.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.orc_exchange_set.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.orc_set_rng_r.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
+        L.orc_rstream_create.restype = C.c_void_p
+        L.orc_rstream_create.argtypes = [C.c_uint32]
+        L.orc_rstream_destroy.argtypes = [C.c_void_p]
+        for fn in ("orc_r_unif", "orc_r_norm", "orc_r_exp", "orc_r_beta11"):
+            getattr(L, fn).restype = C.c_double
+            getattr(L, fn).argtypes = [C.c_void_p]
+        L.orc_r_gamma.restype = C.c_double
+        L.orc_r_gamma.argtypes = [C.c_void_p, C.c_double]
         L.orc_run_csv.argtypes = [C.POINTER(OrcConfig), C.c_char_p, C.c_int, C.c_int, C.c_int]
         _lib = L
     return _lib
@@ -121,6 +130,19 @@ def philox(ctr, key):
     o = (C.c_uint32 * 4)()
     lib().orc_philox4x32_10(c, k, o)
     return list(o)
+
+
+def r_stream(r_seed: int, kind: str, n: int, shape: float = 1.0) -> np.ndarray:
+    """n draws of R's set.seed(r_seed); kind in unif / norm / exp / gamma / beta11."""
+    L = lib()
+    h = L.orc_rstream_create(C.c_uint32(int(r_seed) & 0xFFFFFFFF))
+    try:
+        if kind == "gamma":
+            return np.array([L.orc_r_gamma(h, shape) for _ in range(n)])
+        fn = {"unif": L.orc_r_unif, "norm": L.orc_r_norm, "exp": L.orc_r_exp, "beta11": L.orc_r_beta11}[kind]
+        return np.array([fn(h) for _ in range(n)])
+    finally:
+        L.orc_rstream_destroy(h)
 
 
 def glibc_rand(seed: int, n: int) -> np.ndarray:
@@ -167,7 +189,9 @@ class Oracle:
                  sigma0=0.01, v0E=1e-4, s02E=1e-3, v0G=1e-4, s02G=1e-3,
                  A=1.0, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0,
                  mu0=0.0, sigmaE0=1.0, beta0=None, sigmaGG0=None, eps0=None, comp0=None,
-                 pi0=None, N=None, shard_only=-1):
+                 pi0=None, N=None, shard_only=-1, r_seed=None):
+        # r_seed: draw from the r_compat stream (R's set.seed(r_seed) Mersenne-Twister /
+        # Inversion / rgamma / rbeta, in the reference's call order) instead of Philox
         self._keep = []
         X = np.asfortranarray(np.asarray(X, dtype=np.float64))
         if N is None:
@@ -213,6 +237,8 @@ class Oracle:
         self.h = lib().orc_create(C.byref(cfg))
         if not self.h:
             raise ValueError("orc_create rejected the configuration")
+        if r_seed is not None:
+            lib().orc_set_rng_r(self.h, 1, C.c_uint32(int(r_seed) & 0xFFFFFFFF))
         lib().orc_init(self.h)
 
     def sweep(self, n=1):

@@ -89,6 +89,18 @@ int main(int argc, char **argv) {
     snprintf(tag, sizeof tag, "v2 order %d", m);
     orc_destroy(run(&c, 4, tag));
   }
+  /* r_compat stream (R's generators) through V2 / Horseshoe init and sweeps */
+  for (int model = 0; model < 2; ++model) {
+    orc_config c = base(model ? ORC_HORSESHOE : ORC_V2);
+    c.order_mode = ORC_ORDER_REFERENCE;
+    orc *o = orc_create(&c);
+    if (!o) { fprintf(stderr, "FAILED: orc_create r_compat\n"); exit(1); }
+    CHECK(orc_set_rng_r(o, 1, 2024u));
+    CHECK(orc_init(o));
+    CHECK(orc_sweep(o, 4));
+    printf("%-22s %.12e\n", model ? "hs r_compat" : "v2 r_compat", checksum(o));
+    orc_destroy(o);
+  }
   /* Groups: 3 groups, 2 fixed-effect columns */
   static int32_t gA[NCOL];
   static double cva3[3 * 3];

@@ -12,6 +12,10 @@ summaries by eye (src/BayesRv2.cpp:297-331, src/HorseshoeR.cpp:304-347).
    1.7 % higher (4.4 Monte-Carlo SE); the test bounds every summary by max(4 SE, 3 %) and
    records the sigmaE shift.  The exact multi-GPU alternative is the row-sharded protocol
    (DESIGN.md section 12).
+3. RNG stream: the chain as R would run it -- reference visit order AND R's own generators
+   (the oracle's r_compat stream: Mersenne-Twister, Inversion normals, rgamma, rbeta(1,1), in the
+   reference's call order) -- against the device's Philox + BLOCKED chain; and the Horseshoe the
+   same way.  Within 4 Monte-Carlo SE.
 Fixed seeds: deterministic, not flaky.
 """
 import numpy as np
@@ -76,3 +80,35 @@ def test_column_shards_match_single_shard(oracle_mod, data):
     rel = np.abs(ma - mb) / np.abs(ma)
     assert np.all((z < 4.0) | (rel < 0.03)), (z, rel, ma, mb)
     assert rel[0] < 0.03 and np.all(z[1:] < 4.0), (z, rel)  # sigmaE within 3 %, the rest within 4 SE
+
+
+def test_r_stream_reference_chain_matches_device_chain(oracle_mod, data):
+    O = oracle_mod
+    X, Y, beta, big = data
+    r = _chain(O, X, Y, seed=0, order_mode=O.ORDER_REFERENCE, r_seed=2024)
+    dev = _chain(O, X, Y, seed=31, order_mode=O.ORDER_BLOCKED, block_size=64)
+    z, ma, mb = _compare(r, dev, big)
+    assert np.all(z < 4.0), (z, ma, mb)
+    assert np.all(np.sign(ma[3:]) == np.sign(beta[big]))
+
+
+def test_r_stream_horseshoe_matches_device_chain(oracle_mod, data):
+    O = oracle_mod
+    X, Y, beta, big = data
+
+    def chain(**kw):
+        o = O.Oracle(O.HORSESHOE, X, Y, **HYP, **kw)
+        o.sweep(200)
+        rows = []
+        for _ in range(1500):
+            o.sweep(1)
+            rows.append(np.concatenate([[o.scalar(O.S_SIGMAE), o.scalar(O.S_TAU)], o.vector(O.V_BETA)]))
+        return np.array(rows)
+
+    r = chain(seed=0, order_mode=O.ORDER_REFERENCE, r_seed=99)
+    dev = chain(seed=41, order_mode=O.ORDER_BLOCKED, block_size=64)
+    ma, sa = _mean_se(r)
+    mb, sb = _mean_se(dev)
+    cols = [0] + [2 + j for j in big]  # sigmaE and the large effects (tau: heavy-tailed)
+    z = np.abs(ma - mb)[cols] / np.sqrt(sa ** 2 + sb ** 2)[cols]
+    assert np.all(z < 4.0), (z, ma[cols], mb[cols])

@@ -270,3 +270,41 @@ def test_csv_format(oracle_mod, tmp_path):
     # validation: burn_in > max_iterations -> header only, status 1 (BayesRv2.cpp:69-80)
     assert O.run_csv(p, O.V2, X, Y, 5, 10, 1, cva=CVA, **HYP) == 1
     assert len(open(p).read().splitlines()) == 1
+
+
+# r_compat stream against values R itself prints (R's documented defaults:
+# Mersenne-Twister, Inversion): set.seed(42); runif(3) / set.seed(1); runif(3) /
+# set.seed(1); rnorm(5) / set.seed(123); rnorm(5) / set.seed(42); rnorm(3) / set.seed(1); rexp(3)
+R_KAT = [
+    (42, "unif", [0.9148060, 0.9370754, 0.2861395]),
+    (1, "unif", [0.2655087, 0.3721239, 0.5728534]),
+    (1, "norm", [-0.6264538, 0.1836433, -0.8356286, 1.5952808, 0.3295078]),
+    (123, "norm", [-0.56047565, -0.23017749, 1.55870831, 0.07050839, 0.12928774]),
+    (42, "norm", [1.3709584, -0.5646982, 0.3631284]),
+    (1, "exp", [0.7551818, 1.1816428, 0.1457067]),
+]
+
+
+@pytest.mark.parametrize("seed,kind,vals", R_KAT)
+def test_r_compat_stream_known_answers(oracle_mod, seed, kind, vals):
+    got = oracle_mod.r_stream(seed, kind, len(vals))
+    np.testing.assert_allclose(got, vals, rtol=0, atol=6e-8 if kind != "norm" or seed != 123 else 6e-9)
+
+
+@pytest.mark.parametrize("shape", [0.3, 1.0, 2.5, 7.0, 50.0])
+def test_r_compat_gamma_and_beta_moments(oracle_mod, shape):
+    """rgamma / rbeta(1,1) of the r_compat stream: parity unpinned (no R here), moments only"""
+    g = oracle_mod.r_stream(7, "gamma", 100_000, shape)
+    assert abs(g.mean() - shape) < 5 * np.sqrt(shape / g.size)
+    assert abs(g.var() / shape - 1) < 0.05
+    b = oracle_mod.r_stream(8, "beta11", 100_000)
+    assert abs(b.mean() - 0.5) < 0.005 and abs(b.var() - 1 / 12) < 0.002 and b.min() > 0 and b.max() < 1
+
+
+def test_r_compat_chain_is_deterministic_and_differs_from_philox(oracle_mod):
+    O = oracle_mod
+    X, Y, _ = O.synth_cohort(5, 200, 60, h2=0.5, n_causal=4)
+    run = lambda **kw: O.Oracle(O.V2, X, Y, cva=CVA, order_mode=O.ORDER_REFERENCE, **HYP, **kw).sweep(5)  # noqa: E731
+    a, b, c = run(r_seed=3), run(r_seed=3), run(seed=3)
+    assert np.array_equal(a.vector(O.V_BETA), b.vector(O.V_BETA))
+    assert not np.array_equal(a.vector(O.V_BETA), c.vector(O.V_BETA))
