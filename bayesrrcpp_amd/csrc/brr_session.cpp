@@ -214,6 +214,17 @@ int collect_timing(brr_session *s) {
   return 0;
 }
 
+// this column shard's markers (local indices) in the order the global reference permutation
+// lists them (the unsharded case: the permutation itself)
+std::vector<int32_t> shard_visit(const brr_session *s) {
+  if (s->M_total == s->M && s->col_offset == 0) return s->ref_order;
+  std::vector<int32_t> v;
+  v.reserve((size_t)s->M);
+  for (const int32_t m : s->ref_order)
+    if (m >= s->col_offset && m < s->col_offset + s->M) v.push_back((int32_t)(m - s->col_offset));
+  return v;
+}
+
 int upload_order(brr_session *s, const std::vector<int32_t> &order) {
   // positions s*B+i of the reference order; Gram blocks follow the positions
   std::vector<int32_t> mem((size_t)s->nb * s->B, 0), gi((size_t)s->nb * s->B, 0), bsz(s->nb), gb(s->nb);
@@ -297,7 +308,7 @@ int do_sweep_local(brr_session *s) {
       HIPCHK(hipMemcpyAsync(d.forder, s->ref_forder.data(), (size_t)s->F * 4, hipMemcpyHostToDevice, s->st));
     }
     s->grand.shuffle(s->ref_order);
-    if (int rc = upload_order(s, s->ref_order)) return rc;
+    if (int rc = upload_order(s, shard_visit(s))) return rc;
     HIPCHK(launch_gram(d, 0, d.gram, nullptr, s->st));
     HIPCHK(launch_gram(d, 1, d.xgram, d.xgramT, s->st));
   } else {
@@ -765,10 +776,6 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     set_error("col_offset must be a multiple of block_size when sharded");
     return nullptr;
   }
-  if (opt.shard_count > 1 && opt.order_mode == BRR_ORDER_REFERENCE) {
-    set_error("the reference visit order is defined for a single shard only");
-    return nullptr;
-  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
     set_error("no HIP device available: the MI355X sampler has no CPU fallback");
@@ -939,8 +946,10 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
       return nullptr;
     }
   }
-  s->ref_order.resize((size_t)M);
-  for (int64_t i = 0; i < M; ++i) s->ref_order[(size_t)i] = (int32_t)i;
+  // REFERENCE order: the permutation of ALL M_total markers (every column shard draws the same
+  // glibc stream); a shard visits its own columns in that order (shard_visit)
+  s->ref_order.resize((size_t)M_total);
+  for (int64_t i = 0; i < M_total; ++i) s->ref_order[(size_t)i] = (int32_t)i;
   s->ref_forder.resize((size_t)std::max(s->F, 0));
   for (int i = 0; i < s->F; ++i) s->ref_forder[(size_t)i] = i;
   s->grand.seed(1);  // a fresh process: rand() unseeded == srand(1)

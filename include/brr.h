@@ -45,6 +45,8 @@ enum brr_model { BRR_MODEL_V2 = 0, BRR_MODEL_GROUPS = 1, BRR_MODEL_RESTART = 2, 
  *  REFERENCE the reference's own order: libstdc++ std::random_shuffle driven by glibc
  *            rand() from a fresh-process state (BayesRv2.cpp:182), persisting across
  *            sweeps; Gram blocks are recomputed every sweep (slow; for parity / replay).
+ *            Column shards shuffle the permutation of all M_total markers and visit their own
+ *            columns in its order; row shards visit every marker in it.
  *  IDENTITY  markers 0..P-1 in index order every sweep (debugging). */
 enum brr_order { BRR_ORDER_BLOCKED = 0, BRR_ORDER_REFERENCE = 1, BRR_ORDER_IDENTITY = 2 };
 

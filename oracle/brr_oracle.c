@@ -497,6 +497,7 @@ struct orc {
   double *eps, *ytilde, *beta, *comp, *xsq, *sigmaGG, *pi, *v, *betaAcum, *alpha, *lambda,
       *hsv, *eps_start, *eps_acc;
   int32_t *order, *forder;
+  int32_t *visit;     /* REFERENCE order over column shards: each shard's columns in global order */
   double mu, sigmaE, sigmaF, tau, eta, c2;
   int32_t it;
   glibc_rand grand;
@@ -550,7 +551,7 @@ void orc_destroy(orc *o) {
   if (!o) return;
   free(o->eps); free(o->ytilde); free(o->eps_start); free(o->eps_acc); free(o->beta);
   free(o->comp); free(o->xsq); free(o->lambda); free(o->hsv); free(o->sigmaGG); free(o->pi);
-  free(o->v); free(o->betaAcum); free(o->alpha); free(o->order); free(o->forder);
+  free(o->v); free(o->betaAcum); free(o->alpha); free(o->order); free(o->forder); free(o->visit);
   free(o->stats); free(o->deps);
   orc_rstream_destroy(o->rs);
   free(o);
@@ -679,6 +680,18 @@ static void make_orders(orc *o) {
        * both arrays persist across iterations, exactly like the reference. */
       if (o->F > 0) random_shuffle_ref(&o->grand, o->forder, o->F);
       random_shuffle_ref(&o->grand, o->order, o->P);
+      if (o->c.n_shards > 1) {
+        /* column shards: shard s visits ITS columns in the order the (persisting, global)
+         * permutation lists them -- the reference's order restricted to the shard */
+        if (!o->visit) o->visit = (int32_t *)malloc(sizeof(int32_t) * (size_t)o->P);
+        int64_t pos = 0;
+        for (int sh = 0; sh < o->c.n_shards; ++sh) {
+          int64_t off;
+          const int64_t ps = shard_range(o, sh, &off);
+          for (int64_t i = 0; i < o->P; ++i)
+            if (o->order[i] >= off && o->order[i] < off + ps) o->visit[pos++] = o->order[i];
+        }
+      }
       break;
     case ORC_ORDER_BLOCKED: {
       for (int f = 0; f < o->F; ++f) o->forder[f] = f;
@@ -828,13 +841,14 @@ static void marker_pass(orc *o) {
   memcpy(o->eps_start, o->eps, sizeof(double) * (size_t)N);
   memset(o->eps_acc, 0, sizeof(double) * (size_t)N);
   int64_t pos = 0;
+  const int32_t *ord = (o->c.order_mode == ORC_ORDER_REFERENCE && o->visit) ? o->visit : o->order;
   for (int s = 0; s < o->c.n_shards; ++s) {
     int64_t off;
     int64_t ps = shard_range(o, s, &off);
     if (o->c.shard_only >= 0 && s != o->c.shard_only) { pos += ps; continue; }
     memcpy(o->eps, o->eps_start, sizeof(double) * (size_t)N);
     for (int64_t j = 0; j < ps; ++j) {
-      int64_t m = o->order[pos + j];
+      int64_t m = ord[pos + j];
       if (hs) horseshoe_marker(o, m, o->eps); else bayesr_marker(o, m, o->eps);
     }
     for (int64_t i = 0; i < N; ++i) o->eps_acc[i] += o->eps[i] - o->eps_start[i];

@@ -331,6 +331,53 @@ def test_sharded_two_sessions_match_oracle(brr, oracle_mod, require_gpu):
             assert _rel(s.vector(L.PI), orc.vector(O.V_PI)) < RTOL
 
 
+@pytest.mark.parametrize("model", [0, 1])
+def test_sharded_reference_order_matches_oracle(brr, oracle_mod, require_gpu, model):
+    """REFERENCE visit order over two column shards: every shard draws the same global
+    std::random_shuffle permutation (BayesRv2.cpp:182; Groups: fixedI first, :216) and visits its
+    own columns in that order; host-summed exchange == the oracle's 2-shard emulation."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P, B = 260, 512, 128
+    X, Y, _ = _cohort(O, N, P, n_causal=30)
+    G = 2 if model == L.MODEL_GROUPS else 1
+    gA = (np.arange(P) * G // P).astype(np.int32) if G > 1 else None
+    F = 1 if model == L.MODEL_GROUPS else 0
+    fixed = np.ones((N, 1)) if F else None
+    cva = np.tile(CVA, (G, 1))
+    sess = []
+    for r, (c0, pl) in enumerate([(0, 256), (256, 256)]):
+        s = brr.Session(model, N, pl, K=4, groups=G, F=F, M_total=P, col_offset=c0, block_size=B,
+                        shard_rank=r, shard_count=2, order_mode=L.ORDER_REFERENCE)
+        s.upload_x(X[:, c0:c0 + pl])
+        s.set_y(Y)
+        s.set_bayesr(**HYP, cva=cva, gAssign=gA[c0:c0 + pl] if G > 1 else None)
+        if F:
+            s.set_fixed(fixed)
+        s.init(9)
+        s.exchange_buffers()
+        sess.append(s)
+    orc = O.Oracle({0: O.V2, 1: O.GROUPS}[model], X, Y, cva=cva, G=G, gAssign=gA, fixed=fixed, seed=9,
+                   order_mode=O.ORDER_REFERENCE, block_size=B, n_shards=2, **HYP)
+    for it in range(4):
+        for s in sess:
+            s.sweep_local()
+        parts = [s.exchange_get() for s in sess]
+        te = parts[0][0] + parts[1][0]
+        ts = parts[0][1] + parts[1][1]
+        for s in sess:
+            s.exchange_set(te, ts)
+            s.sweep_finish()
+        orc.sweep(1)
+        comp = np.concatenate([s.vector(L.COMP) for s in sess])
+        beta = np.concatenate([s.vector(L.BETA) for s in sess])
+        assert np.array_equal(comp, orc.vector(O.V_COMP)), f"it={it}"
+        assert _rel(beta, orc.vector(O.V_BETA)) < RTOL
+        for s in sess:
+            assert _rel(s.vector(L.EPS), orc.vector(O.V_EPS)) < RTOL
+            assert _rel([s.scalar(L.SIGMAE)], [orc.scalar(O.S_SIGMAE)]) < RTOL
+
+
 def test_restart_column_shards(brr, oracle_mod, require_gpu):
     """Restart across two column shards: the pi init's component counts (BRv2Grstart.cpp:157-165)
     summed across shards through init_local / exchange / init_finish, then the column-sharded
