@@ -26,6 +26,15 @@ def _cohort(O, N, P, seed=20261015, n_causal=None):
 def _rel(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
+    nf = ~np.isfinite(b)
+    if nf.any():
+        # degenerate draws (e.g. sigmaG = inf from a scaled-inverse-chi^2 with v0G + m0 = 1e-4 degrees
+        # of freedom): the same non-finite value on both sides, the finite rest compared as usual
+        if not np.array_equal(a[nf], b[nf], equal_nan=True):
+            return float("inf")
+        a, b = a[~nf], b[~nf]
+        if not a.size:
+            return 0.0
     scale = np.maximum(np.abs(b), np.max(np.abs(b)) * 1e-3 + 1e-300)
     return float(np.max(np.abs(a - b) / scale)) if a.size else 0.0
 
@@ -679,3 +688,39 @@ def test_session_output_matches_oneshot(brr, oracle_mod, require_gpu, tmp_path, 
             s.output_sample(it)
     assert 1 <= s.output_close() <= depth
     assert open(p1).read() == open(p2).read()
+
+
+@pytest.mark.parametrize("model,N,P,order,kind", [
+    (0, 7, 1, 1, "one marker, 7 rows"),
+    (0, 64, 3, 0, "fewer markers than a wave"),
+    (0, 300, 129, 0, "one full block and a one-marker block"),
+    (0, 257, 200, 1, "K = 2 (one non-zero component)"),
+    (0, 257, 200, 0, "an all-zero and a constant column"),
+    (1, 90, 70, 1, "Groups: G = 3 with an empty group, fixed effect"),
+    (3, 33, 5, 0, "Horseshoe, tiny"),
+])
+def test_edge_shapes(brr, oracle_mod, require_gpu, model, N, P, order, kind):
+    """Edge shapes against the oracle: a single marker, fewer markers or rows than a wave, a ragged
+    one-marker last block, K = 2, degenerate columns (all zero: xsq = 0, BayesRv2.cpp:199; constant),
+    an empty group, a tiny Horseshoe."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    X, Y, _ = _cohort(O, N, P, n_causal=max(1, min(5, P)))
+    cva = CVA
+    kw = {}
+    if "K = 2" in kind:
+        cva = [1e-2]
+    if "degenerate" in kind or "all-zero" in kind:
+        X = np.array(X)
+        X[:, 3] = 0.0
+        X[:, 7] = 0.5
+    if model == L.MODEL_GROUPS:
+        gA = np.where(np.arange(P) < P // 2, 0, 2).astype(np.int32)  # group 1 empty
+        kw = dict(G=3, gAssign=gA, fixed=np.ones((N, 1)))
+    if model == L.MODEL_HORSESHOE:
+        kw = dict(hs=dict(A=1.0, v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0))
+    s, orc = _make(brr, O, model, X, Y, order, cva=cva, **kw)
+    for it in range(4):
+        s.sweep(1)
+        orc.sweep(1)
+        _compare(s, orc, O, L, model, tag=f"{kind} it={it}")
