@@ -505,7 +505,13 @@ def main():
                 "kernel": kname, "avg_launch_us": round(avg_ms * 1e3, 3),
                 "bytes_per_launch": int(bytes_launch),
                 "per_block_us": round(tm["stream_ms"] / max(1, tm["stream_launches"]) * 1e3, 3),
-                "sweep_hbm_gbs": round(x_bytes / (ms * 1e-3) / 1e9, 1)}
+                "sweep_hbm_gbs": round(x_bytes / (ms * 1e-3) / 1e9, 1),
+                # what limits this configuration in measurement; frac is
+                # always against the HBM roofline of the algorithmic bytes
+                "limiter": ("streaming workgroups' 2-bit decode-dot (VALU + LDS), not HBM" if x2 and model != L.MODEL_GROUPS
+                            else "solver workgroup's serial chain" if model == L.MODEL_GROUPS
+                            else "HBM: stream + re-read of every changed column (2x bytes)" if model == L.MODEL_HORSESHOE
+                            else "HBM stream")}
     if args.trace_sweeps:
         # per-sweep wall time and changed markers of a fresh chain's first sweeps (diagnostic)
         tr = []
