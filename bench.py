@@ -508,7 +508,7 @@ def main():
                 "sweep_hbm_gbs": round(x_bytes / (ms * 1e-3) / 1e9, 1),
                 # what limits this configuration in measurement; frac is
                 # always against the HBM roofline of the algorithmic bytes
-                "limiter": ("streaming workgroups' 2-bit decode-dot (VALU + LDS), not HBM" if x2 and model != L.MODEL_GROUPS
+                "limiter": ("streaming workgroups' 2-bit decode-dot: instruction latency at 2 waves per SIMD (VALUBusy ~33 %), not HBM" if x2 and model != L.MODEL_GROUPS
                             else "solver workgroup's serial chain" if model == L.MODEL_GROUPS
                             else "HBM: stream + re-read of every changed column (2x bytes)" if model == L.MODEL_HORSESHOE
                             else "HBM stream")}
