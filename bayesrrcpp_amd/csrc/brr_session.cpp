@@ -938,7 +938,12 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     if (d.lag == 2 && lg && atoi(lg) >= 3 && s->nb >= 5) d.lag = 3;  // (diagnostics: BRR_LAG=3)
     // row shards: the per-block kernels (the cross-shard sum of a block's dots sits between its
     // streaming and its solve; the fused sweep's in-kernel hand-over is one device's)
-    if (rows || (pb && pb[0] == '1') || !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused)) s->fused = FusedCfg{};
+    // 2-bit storage in REFERENCE order: the fused streamers read a block's code tiles in storage
+    // order (whole column blocks), but a REFERENCE block holds arbitrary columns -- the per-block
+    // kernels read each member column by index
+    const bool ref2bit = s->x2bit && s->order_mode == BRR_ORDER_REFERENCE;
+    if (rows || ref2bit || (pb && pb[0] == '1') || !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused))
+      s->fused = FusedCfg{};
     if (s->fused.nsg == 0) d.lag = 1;
     if ((d.lag >= 2 && (s->alloc(&d.xgram2, (int64_t)s->nb * B * B) || s->alloc(&d.xgram2T, (int64_t)s->nb * B * B))) ||
         (d.lag >= 3 && (s->alloc(&d.xgram3, (int64_t)s->nb * B * B) || s->alloc(&d.xgram3T, (int64_t)s->nb * B * B)))) {

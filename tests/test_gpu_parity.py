@@ -340,8 +340,8 @@ def test_sharded_two_sessions_match_oracle(brr, oracle_mod, require_gpu):
             assert _rel(s.vector(L.PI), orc.vector(O.V_PI)) < RTOL
 
 
-@pytest.mark.parametrize("model", [0, 1])
-def test_sharded_reference_order_matches_oracle(brr, oracle_mod, require_gpu, model):
+@pytest.mark.parametrize("model,xs", [(0, "f32"), (1, "f32"), (3, "f32"), (0, "2bit")])
+def test_sharded_reference_order_matches_oracle(brr, oracle_mod, require_gpu, model, xs):
     """REFERENCE visit order over two column shards: every shard draws the same global
     std::random_shuffle permutation (BayesRv2.cpp:182; Groups: fixedI first, :216) and visits its
     own columns in that order; host-summed exchange == the oracle's 2-shard emulation."""
@@ -354,20 +354,28 @@ def test_sharded_reference_order_matches_oracle(brr, oracle_mod, require_gpu, mo
     F = 1 if model == L.MODEL_GROUPS else 0
     fixed = np.ones((N, 1)) if F else None
     cva = np.tile(CVA, (G, 1))
+    hs = dict(A=0.01, v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0)
     sess = []
     for r, (c0, pl) in enumerate([(0, 256), (256, 256)]):
-        s = brr.Session(model, N, pl, K=4, groups=G, F=F, M_total=P, col_offset=c0, block_size=B,
-                        shard_rank=r, shard_count=2, order_mode=L.ORDER_REFERENCE)
+        s = brr.Session(model, N, pl, K=1 if model == L.MODEL_HORSESHOE else 4, groups=G, F=F, M_total=P,
+                        col_offset=c0, block_size=B, shard_rank=r, shard_count=2, order_mode=L.ORDER_REFERENCE,
+                        x_storage=L.X_2BIT if xs == "2bit" else L.X_F32)
         s.upload_x(X[:, c0:c0 + pl])
         s.set_y(Y)
-        s.set_bayesr(**HYP, cva=cva, gAssign=gA[c0:c0 + pl] if G > 1 else None)
+        if model == L.MODEL_HORSESHOE:
+            s.set_horseshoe(**hs)
+        else:
+            s.set_bayesr(**HYP, cva=cva, gAssign=gA[c0:c0 + pl] if G > 1 else None)
         if F:
             s.set_fixed(fixed)
         s.init(9)
         s.exchange_buffers()
         sess.append(s)
-    orc = O.Oracle({0: O.V2, 1: O.GROUPS}[model], X, Y, cva=cva, G=G, gAssign=gA, fixed=fixed, seed=9,
-                   order_mode=O.ORDER_REFERENCE, block_size=B, n_shards=2, **HYP)
+    if model == L.MODEL_HORSESHOE:
+        orc = O.Oracle(O.HORSESHOE, X, Y, seed=9, order_mode=O.ORDER_REFERENCE, block_size=B, n_shards=2, **hs)
+    else:
+        orc = O.Oracle({0: O.V2, 1: O.GROUPS}[model], X, Y, cva=cva, G=G, gAssign=gA, fixed=fixed, seed=9,
+                       order_mode=O.ORDER_REFERENCE, block_size=B, n_shards=2, **HYP)
     for it in range(4):
         for s in sess:
             s.sweep_local()
@@ -378,9 +386,10 @@ def test_sharded_reference_order_matches_oracle(brr, oracle_mod, require_gpu, mo
             s.exchange_set(te, ts)
             s.sweep_finish()
         orc.sweep(1)
-        comp = np.concatenate([s.vector(L.COMP) for s in sess])
         beta = np.concatenate([s.vector(L.BETA) for s in sess])
-        assert np.array_equal(comp, orc.vector(O.V_COMP)), f"it={it}"
+        if model != L.MODEL_HORSESHOE:
+            comp = np.concatenate([s.vector(L.COMP) for s in sess])
+            assert np.array_equal(comp, orc.vector(O.V_COMP)), f"it={it}"
         assert _rel(beta, orc.vector(O.V_BETA)) < RTOL
         for s in sess:
             assert _rel(s.vector(L.EPS), orc.vector(O.V_EPS)) < RTOL
@@ -724,3 +733,40 @@ def test_edge_shapes(brr, oracle_mod, require_gpu, model, N, P, order, kind):
         s.sweep(1)
         orc.sweep(1)
         _compare(s, orc, O, L, model, tag=f"{kind} it={it}")
+
+
+@pytest.mark.parametrize("model", [0, 1, 3])
+def test_2bit_reference_order_matches_oracle(brr, oracle_mod, require_gpu, model):
+    """2-bit storage in the reference's own visit order: a REFERENCE block holds arbitrary
+    columns, so the sweep runs the per-block kernels (each member column decoded by index; the
+    fused streamers read whole column blocks in storage order) -- against the oracle."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P, B = 300, 400, 128
+    X, Y, _ = _cohort(O, N, P, n_causal=30)
+    G = 3 if model == L.MODEL_GROUPS else 1
+    gA = (np.arange(P) * G // P).astype(np.int32) if G > 1 else None
+    hs = dict(A=0.01, v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0)
+    s = brr.Session(model, N, P, K=1 if model == L.MODEL_HORSESHOE else 4, groups=G,
+                    F=1 if model == L.MODEL_GROUPS else 0, block_size=B, order_mode=L.ORDER_REFERENCE,
+                    x_storage=L.X_2BIT)
+    s.upload_x(X)
+    s.set_y(Y)
+    okw = dict(hs)
+    if model == L.MODEL_HORSESHOE:
+        s.set_horseshoe(**hs)
+    else:
+        cva = np.tile(CVA, (G, 1))
+        s.set_bayesr(**HYP, cva=cva, gAssign=gA)
+        okw = dict(HYP, cva=cva, G=G, gAssign=gA)
+        if model == L.MODEL_GROUPS:
+            s.set_fixed(np.ones((N, 1)))
+            okw["fixed"] = np.ones((N, 1))
+    s.init(7)
+    assert s.scalar(104) == 0  # per-block kernels
+    orc = O.Oracle(model, X, Y, seed=7, order_mode=O.ORDER_REFERENCE, block_size=B, **okw)
+    for it in range(4):
+        s.sweep(1)
+        orc.sweep(1)
+        assert np.array_equal(s.vector(L.ORDER), orc.vector(O.V_ORDER)), f"visit order it={it}"
+        _compare(s, orc, O, L, model, tag=f"2bit reference model={model} it={it}")
