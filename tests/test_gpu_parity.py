@@ -301,7 +301,8 @@ def test_oneshot_validation(brr, require_gpu, tmp_path):
     assert open(p).read().startswith("iteration,mu,beta[1]")  # header written before the check
 
 
-def test_sharded_two_sessions_match_oracle(brr, oracle_mod, require_gpu):
+@pytest.mark.parametrize("xs", ["f32", "2bit"])
+def test_sharded_two_sessions_match_oracle(brr, oracle_mod, require_gpu, xs):
     """Column-sharded protocol: two sessions on one GPU, residual deltas and statistics summed
     on the host (the role ncclAllReduce plays across GPUs) == the oracle's 2-shard emulation."""
     from bayesrrcpp_amd import _lib as L
@@ -312,7 +313,7 @@ def test_sharded_two_sessions_match_oracle(brr, oracle_mod, require_gpu):
     sess = []
     for r, (c0, pl) in enumerate(shards):
         s = brr.Session(L.MODEL_V2, N, pl, K=4, M_total=P, col_offset=c0, block_size=B,
-                        shard_rank=r, shard_count=2)
+                        shard_rank=r, shard_count=2, x_storage=L.X_2BIT if xs == "2bit" else L.X_F32)
         s.upload_x(X[:, c0:c0 + pl])
         s.set_y(Y)
         s.set_bayesr(**HYP, cva=CVA)
