@@ -59,12 +59,13 @@ def _compare(sess, orc, O, L, model, tag=""):
 
 
 def _make(brr, O, model, X, Y, order_mode, B=128, G=1, gAssign=None, fixed=None, cva=CVA,
-          seed=7, restart=None, hs=None):
+          seed=7, restart=None, hs=None, xs="f32"):
     from bayesrrcpp_amd import _lib as L
     N, P = X.shape
     K = 1 if model == L.MODEL_HORSESHOE else np.atleast_2d(cva).shape[-1] + 1
     F = 0 if fixed is None else np.asarray(fixed).reshape(N, -1).shape[1]
-    s = brr.Session(model, N, P, K=K, groups=G, F=F, block_size=B, order_mode=order_mode)
+    s = brr.Session(model, N, P, K=K, groups=G, F=F, block_size=B, order_mode=order_mode,
+                    x_storage=L.X_2BIT if xs == "2bit" else L.X_F32)
     s.upload_x(X)
     okw = {}
     if model != L.MODEL_RESTART:
@@ -197,7 +198,8 @@ def test_groups_fixed_effects(brr, oracle_mod, require_gpu):
             assert _rel(s.vector(L.BETAACUM), orc.vector(O.V_BETAACUM)) < RTOL
 
 
-def test_restart(brr, oracle_mod, require_gpu):
+@pytest.mark.parametrize("order,xs", [(0, "f32"), (1, "f32"), (0, "2bit"), (1, "2bit")])
+def test_restart(brr, oracle_mod, require_gpu, order, xs):
     from bayesrrcpp_amd import _lib as L
     O = oracle_mod
     N, P, G = 250, 300, 3
@@ -209,12 +211,12 @@ def test_restart(brr, oracle_mod, require_gpu):
     prev.sweep(4)
     st = dict(mu0=prev.scalar(O.S_MU), beta0=prev.vector(O.V_BETA), sigmaE0=prev.scalar(O.S_SIGMAE),
               sigmaGG0=prev.vector(O.V_SIGMAGG), eps0=prev.vector(O.V_EPS), comp0=prev.vector(O.V_COMP))
-    s, orc = _make(brr, O, L.MODEL_RESTART, X, None, 0, G=G, gAssign=gA, restart=st)
+    s, orc = _make(brr, O, L.MODEL_RESTART, X, None, order, G=G, gAssign=gA, restart=st, xs=xs)
     assert _rel(s.vector(L.PI), orc.vector(O.V_PI)) < RTOL  # Dirichlet(v+1) from components
     for it in range(5):
         s.sweep(1)
         orc.sweep(1)
-        _compare(s, orc, O, L, L.MODEL_RESTART, tag=f"restart it={it}")
+        _compare(s, orc, O, L, L.MODEL_RESTART, tag=f"restart order={order} {xs} it={it}")
 
 
 @pytest.mark.parametrize("order", [0, 1])
