@@ -489,9 +489,10 @@ def test_recycled_device_memory(brr, oracle_mod, require_gpu):
         gc.collect()
 
 
+@pytest.mark.parametrize("xs", ["f32", "2bit"])
 @pytest.mark.parametrize("lag", [1, 2, 3])
-@pytest.mark.parametrize("model", [1, 2, 3])  # Groups, restart, Horseshoe
-def test_pipeline_lag_all_models(brr, oracle_mod, require_gpu, monkeypatch, model, lag):
+@pytest.mark.parametrize("model", [0, 1, 2, 3])  # V2, Groups, restart, Horseshoe
+def test_pipeline_lag_all_models(brr, oracle_mod, require_gpu, monkeypatch, model, lag, xs):
     """Every pipeline lag (default: 2 for V2 / restart on f32, 1 otherwise; 3 is opt-in) for the
     other models, against the oracle: many blocks, several streaming workgroups."""
     from bayesrrcpp_amd import _lib as L
@@ -513,12 +514,13 @@ def test_pipeline_lag_all_models(brr, oracle_mod, require_gpu, monkeypatch, mode
                                eps0=Y - X @ beta0 - 0.01, comp0=comp0))
     elif model == L.MODEL_HORSESHOE:
         kw = dict(hs=dict(A=0.01, v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0))
-    s, orc = _make(brr, O, model, X, Y, 0, B=128, **kw)
+    s, orc = _make(brr, O, model, X, Y, 0, B=128, xs=xs, **kw)
     assert s.scalar(104) > 1  # fused sweep
+    assert s.scalar(106) == lag
     for it in range(4):
         s.sweep(1)
         orc.sweep(1)
-        _compare(s, orc, O, L, model, tag=f"model={model} lag={lag} it={it}")
+        _compare(s, orc, O, L, model, tag=f"model={model} lag={lag} {xs} it={it}")
 
 
 @pytest.mark.parametrize("lag", [1, 2])
