@@ -713,7 +713,8 @@ def test_session_output_matches_oneshot(brr, oracle_mod, require_gpu, tmp_path, 
     (1, 90, 70, 1, "Groups: G = 3 with an empty group, fixed effect"),
     (3, 33, 5, 0, "Horseshoe, tiny"),
 ])
-def test_edge_shapes(brr, oracle_mod, require_gpu, model, N, P, order, kind):
+@pytest.mark.parametrize("xs", ["f32", "2bit"])
+def test_edge_shapes(brr, oracle_mod, require_gpu, model, N, P, order, kind, xs):
     """Edge shapes against the oracle: a single marker, fewer markers or rows than a wave, a ragged
     one-marker last block, K = 2, degenerate columns (all zero: xsq = 0, BayesRv2.cpp:199; constant),
     an empty group, a tiny Horseshoe."""
@@ -733,11 +734,11 @@ def test_edge_shapes(brr, oracle_mod, require_gpu, model, N, P, order, kind):
         kw = dict(G=3, gAssign=gA, fixed=np.ones((N, 1)))
     if model == L.MODEL_HORSESHOE:
         kw = dict(hs=dict(A=1.0, v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0))
-    s, orc = _make(brr, O, model, X, Y, order, cva=cva, **kw)
+    s, orc = _make(brr, O, model, X, Y, order, cva=cva, xs=xs, **kw)
     for it in range(4):
         s.sweep(1)
         orc.sweep(1)
-        _compare(s, orc, O, L, model, tag=f"{kind} it={it}")
+        _compare(s, orc, O, L, model, tag=f"{kind} {xs} it={it}")
 
 
 @pytest.mark.parametrize("model", [0, 1, 3])
