@@ -121,18 +121,19 @@ def test_v2_block64_and_many_sweeps(brr, oracle_mod, require_gpu):
     _compare(s, orc, O, L, L.MODEL_V2, tag="B=64 20 sweeps")
 
 
+@pytest.mark.parametrize("xs", ["f32", "2bit"])
 @pytest.mark.parametrize("B", [256, 512])
-def test_v2_large_blocks(brr, oracle_mod, require_gpu, B):
+def test_v2_large_blocks(brr, oracle_mod, require_gpu, B, xs):
     """Multi-chunk streaming grid, a partial last block, Gram-row slot overflow (sweep 1 changes
     most markers: more candidates than LDS slots) and ragged N (not a multiple of 256 rows)."""
     from bayesrrcpp_amd import _lib as L
     O = oracle_mod
     X, Y, _ = _cohort(O, 301, 1300, n_causal=40)
-    s, orc = _make(brr, O, L.MODEL_V2, X, Y, 0, B=B)
+    s, orc = _make(brr, O, L.MODEL_V2, X, Y, 0, B=B, xs=xs)
     for it in range(5):
         s.sweep(1)
         orc.sweep(1)
-        _compare(s, orc, O, L, L.MODEL_V2, tag=f"B={B} it={it}")
+        _compare(s, orc, O, L, L.MODEL_V2, tag=f"B={B} {xs} it={it}")
 
 
 @pytest.mark.parametrize("mode", ["persistent", "persistent-cap7", "persistent-cap30", "persistent-lag1", "per-block"])
@@ -164,18 +165,19 @@ def test_pipeline_modes_midsize(brr, oracle_mod, require_gpu, monkeypatch, mode)
         _compare(s, orc, O, L, L.MODEL_V2, tag=f"{mode} it={it}")
 
 
-def test_horseshoe_block512(brr, oracle_mod, require_gpu):
+@pytest.mark.parametrize("B,xs", [(512, "f32"), (512, "2bit"), (256, "2bit")])
+def test_horseshoe_block512(brr, oracle_mod, require_gpu, B, xs):
     from bayesrrcpp_amd import _lib as L
     O = oracle_mod
     N, P = 260, 700
     X, Y, _ = _cohort(O, N, P, n_causal=30)
     A = (1 / np.sqrt(N)) * 150 / (P - 150)
     hs = dict(A=A, v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0)
-    s, orc = _make(brr, O, L.MODEL_HORSESHOE, X, Y, 0, B=512, hs=hs)
+    s, orc = _make(brr, O, L.MODEL_HORSESHOE, X, Y, 0, B=B, hs=hs, xs=xs)
     for it in range(4):
         s.sweep(1)
         orc.sweep(1)
-        _compare(s, orc, O, L, L.MODEL_HORSESHOE, tag=f"hs B=512 it={it}")
+        _compare(s, orc, O, L, L.MODEL_HORSESHOE, tag=f"hs B={B} {xs} it={it}")
 
 
 def test_groups_fixed_effects(brr, oracle_mod, require_gpu):
