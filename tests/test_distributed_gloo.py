@@ -20,7 +20,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, model, out_dir):
+def _worker(rank, world, port, model, out_dir, order=0):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -31,7 +31,7 @@ def _worker(rank, world, port, model, out_dir):
     X, Y, _ = O.synth_cohort(11, 240, 384, n_causal=20)
     kw = dict(cva=CVA, **HYP) if model == O.V2 else dict(A=0.01, v0E=1e-3, s02E=1e-3, vL=1, vT=1,
                                                         c2=1, vC=10, sC=10)
-    o = O.Oracle(model, X, Y, seed=3, block_size=64, n_shards=world, shard_only=rank, **kw)
+    o = O.Oracle(model, X, Y, seed=3, block_size=64, n_shards=world, shard_only=rank, order_mode=order, **kw)
     HostExchange(dist).sweep(o, 3)
     np.save(os.path.join(out_dir, f"beta{rank}.npy"), o.vector(O.V_BETA))
     np.save(os.path.join(out_dir, f"eps{rank}.npy"), o.vector(O.V_EPS))
@@ -41,16 +41,16 @@ def _worker(rank, world, port, model, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("model", [0, 3])
-def test_gloo_two_ranks_match_emulation(oracle_mod, tmp_path, model):
+@pytest.mark.parametrize("model,order", [(0, 0), (3, 0), (0, 1), (3, 1)])  # BLOCKED, REFERENCE
+def test_gloo_two_ranks_match_emulation(oracle_mod, tmp_path, model, order):
     import torch.multiprocessing as mp
     O = oracle_mod
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), model, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), model, str(tmp_path), order), nprocs=world, join=True)
     X, Y, _ = O.synth_cohort(11, 240, 384, n_causal=20)
     kw = dict(cva=CVA, **HYP) if model == O.V2 else dict(A=0.01, v0E=1e-3, s02E=1e-3, vL=1, vT=1,
                                                         c2=1, vC=10, sC=10)
-    ref = O.Oracle(model, X, Y, seed=3, block_size=64, n_shards=world, **kw)
+    ref = O.Oracle(model, X, Y, seed=3, block_size=64, n_shards=world, order_mode=order, **kw)
     ref.sweep(3)
     from bayesrrcpp_amd.distributed import shard_columns
     beta = np.zeros(384)
