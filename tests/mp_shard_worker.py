@@ -1,6 +1,7 @@
 """Worker of tests/test_gpu_multiprocess.py: one process per column shard, libbrr session on the
 GPU, residual deltas + statistics summed across processes with torch.distributed (gloo) -- the
-exchange ncclAllReduce performs inside libbrr between GPUs.  argv: rank world port out_dir model."""
+exchange ncclAllReduce performs inside libbrr between GPUs.  argv: rank world port out_dir model
+[order]."""
 import os
 import sys
 
@@ -12,6 +13,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
 
 def main():
     rank, world, port, out_dir, model = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], int(sys.argv[5])
+    order = int(sys.argv[6]) if len(sys.argv) > 6 else 0
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
     import torch
     import torch.distributed as dist
@@ -26,7 +28,7 @@ def main():
     c0, c1 = shard_columns(P, B, rank, world)
     K = 1 if model == L.MODEL_HORSESHOE else len(CVA) + 1
     s = brr.Session(model, N, c1 - c0, K=K, M_total=P, col_offset=c0, block_size=B, shard_rank=rank,
-                    shard_count=world)
+                    shard_count=world, order_mode=order)
     s.upload_x(X[:, c0:c1])
     s.set_y(Y)
     if model == L.MODEL_HORSESHOE:

@@ -26,12 +26,12 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("model", [0, 3])
-def test_two_processes_column_shards(oracle_mod, require_gpu, tmp_path, model):
+@pytest.mark.parametrize("model,order", [(0, 0), (3, 0), (0, 1)])  # BLOCKED; REFERENCE
+def test_two_processes_column_shards(oracle_mod, require_gpu, tmp_path, model, order):
     O = oracle_mod
     world, port = 2, str(_free_port())
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "mp_shard_worker.py"), str(r), str(world), port,
-                               str(tmp_path), str(model)]) for r in range(world)]
+                               str(tmp_path), str(model), str(order)]) for r in range(world)]
     try:
         rcs = [p.wait(timeout=180) for p in procs]
     finally:
@@ -43,7 +43,7 @@ def test_two_processes_column_shards(oracle_mod, require_gpu, tmp_path, model):
     X, Y, _ = O.synth_cohort(20261015, N, P, h2=0.5, n_causal=30)
     kw = dict(cva=CVA, **HYP) if model == O.V2 else dict(A=0.01, v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0,
                                                         c2=1.0, vC=10.0, sC=10.0)
-    ref = O.Oracle(model, X, Y, seed=9, order_mode=O.ORDER_BLOCKED, block_size=B, n_shards=world, **kw)
+    ref = O.Oracle(model, X, Y, seed=9, order_mode=order, block_size=B, n_shards=world, **kw)
     ref.sweep(4)
     beta = np.concatenate([np.load(tmp_path / f"beta{r}.npy") for r in range(world)])
     scale = np.maximum(np.abs(ref.vector(O.V_BETA)), 1e-3 * np.abs(ref.vector(O.V_BETA)).max())
