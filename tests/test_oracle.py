@@ -308,3 +308,15 @@ def test_r_compat_chain_is_deterministic_and_differs_from_philox(oracle_mod):
     a, b, c = run(r_seed=3), run(r_seed=3), run(seed=3)
     assert np.array_equal(a.vector(O.V_BETA), b.vector(O.V_BETA))
     assert not np.array_equal(a.vector(O.V_BETA), c.vector(O.V_BETA))
+
+
+@pytest.mark.parametrize("kind,shape", [("gamma", 0.5), ("gamma", 1.0), ("gamma", 3.3), ("gamma", 20.0),
+                                        ("exp", 1.0), ("beta11", 1.0), ("norm", 1.0)])
+def test_r_compat_distributions_ks(oracle_mod, kind, shape):
+    """The r_compat stream's draws follow their distributions (Kolmogorov-Smirnov against scipy's
+    CDFs, 20,000 draws, fixed seeds): rgamma's GD / GS branches, exp_rand, rbeta(1,1), Inversion."""
+    from scipy import stats
+    x = oracle_mod.r_stream(11, kind, 20_000, shape)
+    cdf = {"gamma": stats.gamma(shape).cdf, "exp": stats.expon().cdf, "beta11": stats.uniform().cdf,
+           "norm": stats.norm().cdf}[kind]
+    assert stats.kstest(x, cdf).pvalue > 1e-3
