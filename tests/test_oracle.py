@@ -320,3 +320,22 @@ def test_r_compat_distributions_ks(oracle_mod, kind, shape):
     cdf = {"gamma": stats.gamma(shape).cdf, "exp": stats.expon().cdf, "beta11": stats.uniform().cdf,
            "norm": stats.norm().cdf}[kind]
     assert stats.kstest(x, cdf).pvalue > 1e-3
+
+
+@pytest.mark.parametrize("shape", [0.3, 1.0, 4.5, 60.0])
+def test_philox_gamma_ks(oracle_mod, shape):
+    """The device's gamma (Marsaglia-Tsang on Philox, boost for a < 1; the GPU's rocRAND engine
+    gives the same words) follows Gamma(shape): Kolmogorov-Smirnov against scipy, 20,000 draws."""
+    from scipy import stats
+    L = oracle_mod.lib()
+    g = np.array([L.orc_gamma(9, shape, 3, i, 0) for i in range(20_000)])
+    assert stats.kstest(g, stats.gamma(shape).cdf).pvalue > 1e-3
+
+
+def test_philox_normal_uniform_ks(oracle_mod):
+    from scipy import stats
+    L = oracle_mod.lib()
+    z = np.array([L.orc_normal(5, 1, i, 0, 1) for i in range(20_000)])
+    u = np.array([L.orc_uniform(5, 1, i, 0, 0) for i in range(20_000)])
+    assert stats.kstest(z, stats.norm().cdf).pvalue > 1e-3
+    assert stats.kstest(u, stats.uniform().cdf).pvalue > 1e-3
