@@ -14,6 +14,7 @@
 #include <map>
 #include <memory>
 #include <condition_variable>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -242,9 +243,16 @@ int run_chain(brr_session *s, const Run &r, CsvWriter *w) {
   return 0;
 }
 
+// an ABI-1 caller's struct ends before the row-shard fields (as in brr_session_create): copy only
+// what it holds over the defaults
 brr_options opts_or_default(const brr_options *o) {
   brr_options r;
-  if (o) r = *o; else brr_options_default(&r);
+  brr_options_default(&r);
+  if (o) {
+    if (o->abi_version >= 2) r = *o;
+    else std::memcpy(&r, o, offsetof(brr_options, row_shard_rank));
+    r.abi_version = BRR_ABI_VERSION;
+  }
   return r;
 }
 

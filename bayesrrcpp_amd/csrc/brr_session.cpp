@@ -287,6 +287,9 @@ int check_device_error(brr_session *s) {
 
 int ensure_reduced(brr_session *s) {
   if (!s->need_reduce) return 0;
+  // row shards: S1/S2 run over every shard's rows; a local reduce here would leave this shard's
+  // partial sums marked as final.  coll_sweep_rows reduces and sums them across shards.
+  if (s->nrshard > 1) return 0;
   s->need_reduce = false;
   return rows_flagged(s, H_ROW_REDUCE);
 }
@@ -768,8 +771,10 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   // B = 128 / 256 / 512)
   // (small cohorts: the chain, not the stream, dominates every sampler -- C1, N = 2,000: 147 against
   // 90 sweeps/s at B = 128 / 512 -- so B = 128 below N = 32,768)
+  // (row shards choose from the cohort's N_total: every shard must run the same B, and the same B
+  // as the unsharded chain)
   int B = opt.block_size > 0 ? opt.block_size
-                             : ((model == MODEL_HORSESHOE || model == MODEL_GROUPS || N < 32768) ? 128 : 512);
+                             : ((model == MODEL_HORSESHOE || model == MODEL_GROUPS || N_total < 32768) ? 128 : 512);
   if (B % 64 != 0 || B > BMAX) { set_error("block_size=%d must be a multiple of 64 and <= %d", B, BMAX); return nullptr; }
   if (opt.shard_count < 1) opt.shard_count = 1;
   if (opt.shard_count > 1 && (col_offset % B) != 0) {
@@ -961,7 +966,13 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   return s;
 }
 
-void brr_session_destroy(brr_session *s) { delete s; }
+void brr_session_destroy(brr_session *s) {
+  if (!s) return;
+  // an output still open (brr_session_output_open without _close, e.g. after an error in the
+  // caller): join its writer thread and drain its rows before the sample ring goes away
+  (void)brr_session_output_close(s, nullptr);
+  delete s;
+}
 
 // 2-bit encoding of columns c0 .. c0+nc-1 of a host matrix (f64 or f32, leading dimension ldx):
 // each column's distinct f32 values plus 0 (the padding rows) must number at most 4; codes are
@@ -1747,24 +1758,33 @@ int sample_ring_push(brr_session *s, int *slot_out) {
     r.next = (r.next + 1) % r.depth;
     r.max_in_use = std::max(r.max_in_use, ++r.in_use);
   }
-  HIPCHK(hipSetDevice(s->device));
-  if (int rc = ensure_reduced(s)) return rc;
-  char *d = r.dbuf[slot];
-  const Dev &dv = s->d;
-  auto cp = [&](size_t off, const void *src, size_t n) {
-    return n ? hipMemcpyAsync(d + off, src, n, hipMemcpyDeviceToDevice, s->st) : hipSuccess;
+  // the snapshot and its copy; on any failure the claimed slot goes back to the ring (a failing
+  // push must not shrink the ring until a later push blocks for ever)
+  auto enqueue = [&]() -> int {
+    HIPCHK(hipSetDevice(s->device));
+    if (int rc = ensure_reduced(s)) return rc;
+    char *d = r.dbuf[slot];
+    const Dev &dv = s->d;
+    auto cp = [&](size_t off, const void *src, size_t n) {
+      return n ? hipMemcpyAsync(d + off, src, n, hipMemcpyDeviceToDevice, s->st) : hipSuccess;
+    };
+    HIPCHK(cp(0, dv.sc, sizeof(Scal)));
+    HIPCHK(cp(r.o_beta, dv.beta, 8 * (size_t)s->M));
+    HIPCHK(cp(r.o_eps, dv.eps, 8 * (size_t)s->N));
+    if (s->model == MODEL_HORSESHOE) HIPCHK(cp(r.o_lam, dv.lambda, 8 * (size_t)s->M));
+    HIPCHK(cp(r.o_sgg, dv.sigmaGG, 8 * (size_t)s->G));
+    if (s->F > 0) HIPCHK(cp(r.o_alpha, dv.alpha, 8 * (size_t)s->F));
+    HIPCHK(cp(r.o_comp, dv.comp, 4 * (size_t)s->M));
+    HIPCHK(hipEventRecord(r.ev_snap[slot], s->st));
+    HIPCHK(hipStreamWaitEvent(r.cst, r.ev_snap[slot], 0));
+    HIPCHK(hipMemcpyAsync(r.hbuf[slot], d, r.bytes, hipMemcpyDeviceToHost, r.cst));
+    HIPCHK(hipEventRecord(r.ev_host[slot], r.cst));
+    return 0;
   };
-  HIPCHK(cp(0, dv.sc, sizeof(Scal)));
-  HIPCHK(cp(r.o_beta, dv.beta, 8 * (size_t)s->M));
-  HIPCHK(cp(r.o_eps, dv.eps, 8 * (size_t)s->N));
-  if (s->model == MODEL_HORSESHOE) HIPCHK(cp(r.o_lam, dv.lambda, 8 * (size_t)s->M));
-  HIPCHK(cp(r.o_sgg, dv.sigmaGG, 8 * (size_t)s->G));
-  if (s->F > 0) HIPCHK(cp(r.o_alpha, dv.alpha, 8 * (size_t)s->F));
-  HIPCHK(cp(r.o_comp, dv.comp, 4 * (size_t)s->M));
-  HIPCHK(hipEventRecord(r.ev_snap[slot], s->st));
-  HIPCHK(hipStreamWaitEvent(r.cst, r.ev_snap[slot], 0));
-  HIPCHK(hipMemcpyAsync(r.hbuf[slot], d, r.bytes, hipMemcpyDeviceToHost, r.cst));
-  HIPCHK(hipEventRecord(r.ev_host[slot], r.cst));
+  if (int rc = enqueue()) {
+    sample_ring_release(s, slot);
+    return rc;
+  }
   *slot_out = slot;
   return 0;
 }

@@ -215,3 +215,49 @@ def test_rowshard_synthetic_cohort_matches_unsharded(brr, oracle_mod, require_gp
     assert _rel(ms[0].vector(L.BETA), one.vector(L.BETA)) < RTOL
     assert _rel(np.concatenate([m.vector(L.EPS) for m in ms]), one.vector(L.EPS)) < RTOL
     g.close()
+
+
+def test_rowshard_automatic_block_size_from_cohort(brr, oracle_mod, require_gpu):
+    """block_size = 0 picks B from the cohort's N_total on every shard: a cohort split
+    across the N = 32,768 boundary (40k + 24k rows) runs B = 512 on both shards, as the unsharded
+    chain does, and matches the unsharded oracle."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P = 64_000, 600
+    X, Y, _ = O.synth_cohort(20261015, N, P, h2=0.5, n_causal=30)
+    cuts = [0, 40_000, N]
+    g, ms, orc = _build(brr, O, L.MODEL_V2, X, Y, cuts, 0, B=0)
+    assert [m.block_size for m in ms] == [512, 512]
+    for it in range(2):
+        g.sweep(1)
+        orc.sweep(1)
+        _compare(ms, orc, O, L, L.MODEL_V2, f"auto-B it={it}")
+    g.close()
+
+
+def test_rowshard_set_state_then_read_then_sweep(brr, oracle_mod, require_gpu):
+    """set_vector(EPS) / set_scalar(MU) on every shard, a state read (which used to reduce the
+    residual sums over this shard's rows only and mark them final), then a group sweep: the
+    residual sums must still be summed across the shards."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P = 900, 512
+    X, Y, _ = O.synth_cohort(20261015, N, P, h2=0.5, n_causal=30)
+    cuts = [0, 380, N]
+    g, ms, orc = _build(brr, O, L.MODEL_V2, X, Y, cuts, 0)
+    g.sweep(2)
+    orc.sweep(2)
+    eps = orc.vector(O.V_EPS) + 0.01 * np.sin(np.arange(N))
+    mu = orc.scalar(O.S_MU) + 0.05
+    orc.set_vector(O.V_EPS, eps)
+    orc.set_scalar(O.S_MU, mu)
+    for m, a, b in zip(ms, cuts[:-1], cuts[1:]):
+        m.set_vector(L.EPS, eps[a:b])
+        m.set_scalar(L.MU, mu)
+    ms[0].scalar(L.MU)  # a read between the setters and the sweep
+    ms[1].vector(L.BETA)
+    for it in range(2):
+        g.sweep(1)
+        orc.sweep(1)
+        _compare(ms, orc, O, L, L.MODEL_V2, f"set-eps it={it}")
+    g.close()
