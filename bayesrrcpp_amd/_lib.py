@@ -16,7 +16,7 @@ ORDER_BLOCKED, ORDER_REFERENCE, ORDER_IDENTITY = 0, 1, 2
 X_F32, X_2BIT = 0, 1  # brr_x_storage
 (MU, SIGMAE, SIGMAG, SIGMAF, TAU, ETA, C2, SUMSQ_BETA) = range(8)
 (BETA, COMP, EPS, SIGMAGG, PI, ALPHA, LAMBDA, XSQ, ORDER, VCOUNT, BETAACUM, HSV) = range(12)
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 LOG_FN = C.CFUNCTYPE(None, C.c_char_p, C.c_void_p)
 
@@ -33,6 +33,7 @@ class Options(C.Structure):
         ("log", LOG_FN), ("log_userdata", C.c_void_p),
         ("row_shard_rank", C.c_int32), ("row_shard_count", C.c_int32),
         ("row_offset", C.c_int64), ("N_total", C.c_int64),
+        ("exchanges_per_sweep", C.c_int32),
     ]
 
 
@@ -48,7 +49,7 @@ EXPORTED = [
     "brr_session_exchange_sizes", "brr_session_set_exchange", "brr_session_exchange_buffers",
     "brr_session_exchange_copy", "brr_comm_unique_id", "brr_session_comm_init",
     "brr_session_sweep_local", "brr_session_init_local", "brr_session_init_finish",
-    "brr_session_sweep_finish", "brr_session_get_scalar", "brr_session_get_vector",
+    "brr_session_sweep_finish", "brr_session_exchanges_per_sweep", "brr_session_get_scalar", "brr_session_get_vector",
     "brr_session_set_vector", "brr_session_set_scalar", "brr_session_iteration",
     "brr_session_set_timing", "brr_session_timing", "brr_session_block_size",
     "brr_session_synchronize", "brr_session_linear_predictor",
@@ -118,6 +119,8 @@ def lib():
     L.brr_session_init_local.argtypes = [vp, C.c_int32]
     L.brr_session_init_finish.argtypes = [vp]
     L.brr_session_sweep_finish.argtypes = [vp]
+    L.brr_session_exchanges_per_sweep.restype = C.c_int32
+    L.brr_session_exchanges_per_sweep.argtypes = [vp]
     L.brr_session_get_scalar.argtypes = [vp, C.c_int32, D]
     L.brr_session_get_vector.restype = C.c_int64
     L.brr_session_get_vector.argtypes = [vp, C.c_int32, D]
@@ -157,7 +160,7 @@ def check(rc: int, what: str) -> int:
 
 def options(device=0, block_size=0, order_mode=ORDER_BLOCKED, shard_rank=0, shard_count=1,
             verbose=0, log=None, x_storage=X_F32, row_shard_rank=0, row_shard_count=1, row_offset=0,
-            N_total=0) -> Options:
+            N_total=0, exchanges_per_sweep=1) -> Options:
     o = Options()
     lib().brr_options_default(C.byref(o))
     o.device, o.block_size, o.order_mode = device, block_size, order_mode
@@ -165,6 +168,7 @@ def options(device=0, block_size=0, order_mode=ORDER_BLOCKED, shard_rank=0, shar
     o.x_storage = x_storage
     o.row_shard_rank, o.row_shard_count = row_shard_rank, row_shard_count
     o.row_offset, o.N_total = row_offset, N_total
+    o.exchanges_per_sweep = exchanges_per_sweep
     if log is not None:
         cb = LOG_FN(lambda msg, _u: log(msg.decode()))
         o.log = cb

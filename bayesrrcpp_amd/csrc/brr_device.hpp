@@ -95,6 +95,8 @@ struct Dev {
   int64_t N, ld, M, M_total, col_offset;
   int64_t Ntot, row_offset;  // row shards: cohort rows and this shard's first row (else N, 0)
   int K, G, F, B, nb, model, R, RG, NG, MRG;
+  int seg0, seg1;   // block positions of the current marker-loop launch(es): [seg0, seg1) (the
+                    // sweep: [0, nb); a column-shard exchange segment: a part, brr_options)
   int gtarget;      // reduction groups k_solve(s) waits for (per-block: NG * NC; persistent: NG)
   int slab_storage; // the partial dots are indexed by in-block storage index, not visit position
                     // (fused sweep on 2-bit code tiles)

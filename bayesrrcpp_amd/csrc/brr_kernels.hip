@@ -1030,7 +1030,7 @@ __global__ __launch_bounds__(256, 2) void k_stream(Dev d, int s, const double *e
   // residual update for block s-2, eps = (eps + x b_old) - x b_new (BayesRv2.cpp:191,243): wait
   // until k_solve(s-2) has published (normally long done), then read its list with sc1 loads;
   // lists are padded to a multiple of 16 with neutral b_old = b_new = 0
-  if (s >= 2) {
+  if (s >= d.seg0 + 2) {  // (blocks before the launch's first are in eps_in already)
     // one wave stages the list in LDS (one sc1 request per line per workgroup, instead of one
     // per wave and entry hammering the same few lines from every workgroup)
     if (w == 0) {
@@ -1566,10 +1566,10 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   const bool resident = B <= RESIDENT_BMAX && nslot >= B + solve_scratch_rows(B, NT);
   // misc[10] / misc[11]: padded length / block of the change list this workgroup left in LDS;
   // misc[12]: block whose Gram copy into LDS the previous block already started
-  if (t == 0 && s == 0) { misc[11] = -2; misc[12] = -2; }
+  if (t == 0 && s == d.seg0) { misc[11] = -2; misc[12] = -2; }
   const bool pipelined = persistent && resident;
-  const int gi_t = (pipelined && s >= 1) ? gi_pref : (t % B < bs ? d.gidx[q0 + t % B] : 0);
-  if (pipelined && s + 1 < d.nb) gi_pref = d.gidx[(int64_t)(s + 1) * B + t % B];
+  const int gi_t = (pipelined && s > d.seg0) ? gi_pref : (t % B < bs ? d.gidx[q0 + t % B] : 0);
+  if (pipelined && s + 1 < d.seg1) gi_pref = d.gidx[(int64_t)(s + 1) * B + t % B];
 
   // A) everything that does not depend on k_stream(s).  The per-position constants are loaded
   // first (vmcnt retires loads in order, so loads issued behind the 128 KiB Gram copy would wait
@@ -1603,7 +1603,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       }
     }
   }
-  if (resident && !(pipelined && s >= 1 && misc[12] == s)) {
+  if (resident && !(pipelined && s > d.seg0 && misc[12] == s)) {
     // row gi at slots + gi B, 1 KiB per wave-instruction; retired by each wave's vmcnt(0) and the
     // barrier after it (before the coefficients / decisions read it).  (The persistent solver
     // starts this copy at the end of the previous block already, see step 3.)
@@ -1617,7 +1617,8 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   const uint64_t tA1 = prof ? wall_clock64() : 0;  // constants loaded (this thread's)
   // sum_i (x_j . x_i) delta_i over the changes of the blocks the streamed dots have not seen:
   // block s-1 (cross-Gram of cycle neighbours), and with lag 2 also block s-2 (cross-Gram of
-  // blocks two apart), added in that order.  Each change list (padded to a multiple of 16) is
+  // blocks two apart), added in that order -- blocks of this launch only (seg0 onwards: the
+  // earlier ones' changes are in the residual the launch started from).  Each change list (padded to a multiple of 16) is
   // staged in the slot area, which is free until step 2; with B < NT the NT / B thread groups
   // take contiguous parts of a list and their partial sums are added in group order.
   constexpr int PG = B < NT ? NT / B : 1;
@@ -1628,11 +1629,11 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   const int nlist = d.lag;
   for (int l = 0; l < nlist; ++l) {
     const int sp = s - 1 - l;  // the earlier block
-    if (l > 0 && sp < 0) break;
+    if (l > 0 && sp < d.seg0) break;
     if (l > 0) __syncthreads();  // every thread is done with the previous list's staging / partials
     const double *C = nullptr;
     int np_prev = 0;
-    if (sp >= 0) {
+    if (sp >= d.seg0) {
       const int gp = d.gblk[sp];
       if (l == 0)
         C = (gb == (gp + 1) % d.nb) ? d.xgram + (int64_t)gp * B * B : d.xgramT + (int64_t)gb * B * B;
@@ -1640,7 +1641,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
         C = (gb == (gp + 2) % d.nb) ? d.xgram2 + (int64_t)gp * B * B : d.xgram2T + (int64_t)gb * B * B;
       else
         C = (gb == (gp + 3) % d.nb) ? d.xgram3 + (int64_t)gp * B * B : d.xgram3T + (int64_t)gb * B * B;
-      if (persistent && resident && l == 0 && s >= 1 && misc[11] == s - 1) {
+      if (persistent && resident && l == 0 && s > d.seg0 && misc[11] == s - 1) {
         // this workgroup wrote block s-1's list into Lcg / Lcd itself (step 4 of that block,
         // persistent solver): no global round trip
         np_prev = misc[10];
@@ -2055,7 +2056,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   __syncthreads();
   if (prof) tp3 = wall_clock64();
   const uint64_t tc3 = prof ? __builtin_amdgcn_s_memtime() : 0;
-  if (BRR_EARLY_GRAM && pipelined && s + 1 < d.nb) {
+  if (BRR_EARLY_GRAM && pipelined && s + 1 < d.seg1) {
     // this block's coefficients are no longer read: the upper half of the waves starts copying
     // the next block's Gram block into LDS, in flight during the write-back and the next block's
     // constants and cross-Gram loads.  (Measured slower: every barrier of the write-back then waits
@@ -2465,13 +2466,16 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       }
     }
   };
+  // this launch's block positions [sb0, sb1): the sweep, or one exchange segment of it
+  const int sb0 = d.seg0, sb1 = d.seg1;
   for (int i = t; i < npass * SROWS; i += SWEEP_NT) eps_l[i] = r0 + i < r1 ? d.eps[r0 + i] : 0.0;
-  stage_lut(0);
-  if (nb > 1) stage_lut(1);
+  stage_lut(sb0);
+  if (sb0 + 1 < sb1) stage_lut(sb0 + 1);
   // f32 path: the member (column) indices of blocks s and s + 1 live in LDS (s_mem[(s & 1) B ..]),
   // so an item's loads need no scalar-cache miss first; block s + 1's are copied at boundary s
   if constexpr (!XF)
-    for (int i = t; i < min(2, nb) * B; i += SWEEP_NT) s_mem[i] = d.member[i];
+    for (int i = t; i < min(2, sb1 - sb0) * B; i += SWEEP_NT)
+      s_mem[(((sb0 + i / B) & 1) * B) + i % B] = d.member[(int64_t)sb0 * B + i];
   __syncthreads();
   const int CPW = B / SWEEP_NW;  // columns per wave
   const int NCH = CPW / CW;      // chunks per wave and block
@@ -2482,7 +2486,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     return (XF && s_codes) ? s_codes + (int64_t)(s % NCC) * B * (npass * 64) : nullptr;
   };
   const int items = NCH * npass; // (chunk, pass) items per wave and block
-  const int total = items * nb;
+  const int total = items * (sb1 - sb0);
   const int grp = g / FUSED_GROUP;
   // Lanes whose 4 rows start at or beyond r1 re-read the workgroup's first rows (their
   // residual rows are 0, so they add exactly 0); rows in [N, ld) are zero padding of X.  The
@@ -2493,7 +2497,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   using Raw = typename std::conditional<XF != 0, uint4, float4>::type;
   constexpr int NR = XF ? 1 : CW;
   auto issue = [&](int it, Raw (&x)[NR]) {
-    const int s = it / items, rem = it - s * items;
+    const int s = sb0 + it / items, rem = it - (s - sb0) * items;
     const int c = rem / npass, p = rem - c * npass;
     const int64_t off = r0 + p * SROWS + 4 * lane < r1 ? r0 + p * SROWS + 4 * lane : r0;
     if constexpr (XF) {
@@ -2532,17 +2536,18 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   // at a chunk's last pass; block_end(it, s, xn): the prefetch into xn issued after the partial-dot
   // stores, their drain and the group-counter arrival.
   auto boundary = [&](int s) __attribute__((always_inline)) {
-    if (s >= 1 && s <= LAG) {
+    const int sr = s - sb0;  // position in this launch
+    if (sr >= 1 && sr <= LAG) {
       // a boundary without a change list to apply yet: stage block s+1's tables / indices
       if constexpr (XF) {
-        if (s + 1 < nb) stage_lut(s + 1);  // (its buffer is not read before the barrier)
-      } else if (s + 1 < nb) {
+        if (s + 1 < sb1) stage_lut(s + 1);  // (its buffer is not read before the barrier)
+      } else if (s + 1 < sb1) {
         __syncthreads();  // every wave is done issuing block s-1's items (same member buffer)
         for (int i = t; i < B; i += SWEEP_NT) s_mem[((s + 1) & 1) * B + i] = d.member[(int64_t)(s + 1) * B + i];
       }
       __syncthreads();
     }
-    if (s >= LAG + 1) {
+    if (sr >= LAG + 1) {
       // block boundary: apply block a = s-1-LAG's changes to the residual rows (lag 1: they
       // then hold every change before block s-1, which the solver corrects for through the
       // cross-Gram; lag 2: before block s-2, corrected for blocks s-2 and s-1)
@@ -2558,10 +2563,10 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
         }
       }
       apply_pending<XF>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, s_part,
-                        (!XF && s + 1 < nb) ? d.member + (int64_t)(s + 1) * B : nullptr, s_mem + ((s + 1) & 1) * B,
+                        (!XF && s + 1 < sb1) ? d.member + (int64_t)(s + 1) * B : nullptr, s_mem + ((s + 1) & 1) * B,
                         cache_of(a), s_mem,
-                        (XF && s + 1 < nb) ? reinterpret_cast<const float4 *>(d.xlut) + (int64_t)d.gblk[s + 1] * B : nullptr,
-                        lut_of(s + 1), lut_of(a), (XF && s + 1 < nb) ? d.bsz[s + 1] : 0,
+                        (XF && s + 1 < sb1) ? reinterpret_cast<const float4 *>(d.xlut) + (int64_t)d.gblk[s + 1] * B : nullptr,
+                        lut_of(s + 1), lut_of(a), (XF && s + 1 < sb1) ? d.bsz[s + 1] : 0,
                         (prof && t == 0) ? acc_sub : nullptr);
       if (prof && t == 0) {
         tr_last(d, s, TR_APPLY_LAST);
@@ -2573,7 +2578,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     }
   };
   auto consume = [&](int it, const Raw (&xc)[NR]) __attribute__((always_inline)) {
-    const int s = it / items, rem = it - s * items;
+    const int s = sb0 + it / items, rem = it - (s - sb0) * items;
     const int c = rem / npass, p = rem - c * npass;
     const double *e = eps_l + p * SROWS + 4 * lane;
     const double e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
@@ -2654,7 +2659,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       static_for<R>([&](auto uc) __attribute__((always_inline)) {
         constexpr int u = decltype(uc)::value;
         const int it = it0 + u;
-        const int s = it / items, rem = it - s * items;
+        const int s = sb0 + it / items, rem = it - (s - sb0) * items;
         if constexpr (u == 0)
           if (rem == 0) boundary(s);
         const bool blk_end = u == R - 1 && rem == items - 1;
@@ -2667,7 +2672,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   } else {
     for (int it = 0; it < total; ++it) {
-      const int s = it / items, rem = it - s * items;
+      const int s = sb0 + it / items, rem = it - (s - sb0) * items;
       const bool blk_end = rem == items - 1;
       if (rem == 0) boundary(s);
       // prefetch P items ahead (across block boundaries) before consuming this one; at a block's
@@ -2691,9 +2696,9 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     acc[5120 + g] = acc_sub[2];
     acc[6144 + g] = acc_sub[3];
   }
-  // end of sweep: the last LAG + 1 blocks' changes, then the residual rows back to HBM
-  if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + nb, d.sync, 4);
-  for (int a = max(0, nb - 1 - LAG); a < nb; ++a)
+  // end of the launch: the last LAG + 1 blocks' changes, then the residual rows back to HBM
+  if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + sb1, d.sync, 4);
+  for (int a = max(sb0, sb1 - 1 - LAG); a < sb1; ++a)
     apply_pending<XF>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, s_part, nullptr, nullptr, cache_of(a),
                       s_mem, nullptr, nullptr, lut_of(a));
   for (int i = t; i < npass * SROWS; i += SWEEP_NT)
@@ -2708,7 +2713,7 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
   const int t = threadIdx.x;
   const int ng = (nsg + FUSED_GROUP - 1) / FUSED_GROUP;
   const int B = d.B;
-  for (int s = 0; s < d.nb; ++s) {
+  for (int s = d.seg0; s < d.seg1; ++s) {
     const int par = s % NPAR;
     const int use = d.gbase[par] + s / NPAR;
     const double *slab1 = d.slab1 + par * d.slab1_stride;
@@ -2731,10 +2736,18 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
   }
 }
 
+#ifndef BRR_SOLVER_CALL
+#define BRR_SOLVER_CALL 0  // (diagnostics) the solver role as a called function: its own register allocation
+#endif
+#if BRR_SOLVER_CALL
+#define BRR_SOLVER_INL __attribute__((noinline))
+#else
+#define BRR_SOLVER_INL __forceinline__
+#endif
 template <bool HS, int B>
-__device__ __forceinline__ void solver_role(const Dev &d, uint32_t it, int nslot, char *smem) {
+__device__ BRR_SOLVER_INL void solver_role(const Dev &d, uint32_t it, int nslot, char *smem) {
   int gi_pref = 0;
-  for (int s = 0; s < d.nb; ++s) {
+  for (int s = d.seg0; s < d.seg1; ++s) {
     solve_block<HS, B, SWEEP_NT>(d, s, it, nslot, smem, true, gi_pref);
     __syncthreads();
   }

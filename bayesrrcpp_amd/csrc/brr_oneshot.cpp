@@ -243,18 +243,7 @@ int run_chain(brr_session *s, const Run &r, CsvWriter *w) {
   return 0;
 }
 
-// an ABI-1 caller's struct ends before the row-shard fields (as in brr_session_create): copy only
-// what it holds over the defaults
-brr_options opts_or_default(const brr_options *o) {
-  brr_options r;
-  brr_options_default(&r);
-  if (o) {
-    if (o->abi_version >= 2) r = *o;
-    else std::memcpy(&r, o, offsetof(brr_options, row_shard_rank));
-    r.abi_version = BRR_ABI_VERSION;
-  }
-  return r;
-}
+brr_options opts_or_default(const brr_options *o) { return brr::options_from_caller(o); }
 
 }  // namespace
 

@@ -10,6 +10,7 @@
 #pragma once
 #include <stdint.h>
 
+#include "../../include/brr.h"
 #include "brr_device.hpp"
 
 struct brr_session;
@@ -32,5 +33,9 @@ int sample_ring_wait(brr_session *s, int slot, SampleView *v);  // its host copy
 void sample_ring_release(brr_session *s, int slot);
 void sample_ring_close(brr_session *s);
 int sample_ring_max_in_use(brr_session *s);  // diagnostics: most slots ever taken at once
+
+// a caller's options over the defaults, by the caller's ABI version: an older caller's struct
+// ends before the fields a later ABI added (ABI 1: row shards, ABI 2: exchanges_per_sweep)
+brr_options options_from_caller(const brr_options *in);
 
 }  // namespace brr

@@ -142,6 +142,7 @@ struct brr_session {
   int K = 1, G = 1, F = 0, B = 128, nb = 0, model = 0, NS = 0;
   int order_mode = BRR_ORDER_BLOCKED;
   int shard = 0, nshard = 1;
+  int nex = 1, seg = 0;         // column shards: exchanges per sweep, the sweep's current segment
   int rshard = 0, nrshard = 1;  // exact row shards: this session's rank / count
   hipEvent_t ev_x = nullptr;    // row shards in one process (brr_group): cross-stream ordering
   int32_t iteration = 0;
@@ -294,49 +295,65 @@ int ensure_reduced(brr_session *s) {
   return rows_flagged(s, H_ROW_REDUCE);
 }
 
+// block positions [seg0, seg1) of exchange segment e of E (whole blocks; the oracle splits a
+// shard's positions the same way, oracle/brr_oracle.c seg_positions)
+void seg_range(int nb, int e, int E, int *seg0, int *seg1) {
+  *seg0 = (int)((int64_t)nb * e / E);
+  *seg1 = (int)((int64_t)nb * (e + 1) / E);
+}
+
 int do_sweep_local(brr_session *s) {
   if (!s->initialized) { set_error("session not initialised (brr_session_init)"); return -1; }
   if (int rc = ensure_reduced(s)) return rc;
   const uint32_t it = (uint32_t)s->iteration;
   const bool sharded = s->nshard > 1;
+  const bool last = s->seg == s->nex - 1;
   Dev &d = s->d;
-  HIPCHK(launch_sweep_start(d, it, s->st));
-  if (int rc = rows_flagged(s, H_ROW_SHIFT | H_ROW_WRITE)) return rc;
-  // visit order
-  if (s->order_mode == BRR_ORDER_BLOCKED) {
-    HIPCHK(launch_perm(d, it, s->shard, false, s->st));
-  } else if (s->order_mode == BRR_ORDER_REFERENCE) {
-    if (s->F > 0) {  // fixedI shuffled before markerI (BayesRv2Groups.cpp:216,227)
-      s->grand.shuffle(s->ref_forder);
-      HIPCHK(hipMemcpyAsync(d.forder, s->ref_forder.data(), (size_t)s->F * 4, hipMemcpyHostToDevice, s->st));
+  if (s->seg == 0) {
+    HIPCHK(launch_sweep_start(d, it, s->st));
+    if (int rc = rows_flagged(s, H_ROW_SHIFT | H_ROW_WRITE)) return rc;
+    // visit order
+    if (s->order_mode == BRR_ORDER_BLOCKED) {
+      HIPCHK(launch_perm(d, it, s->shard, false, s->st));
+    } else if (s->order_mode == BRR_ORDER_REFERENCE) {
+      if (s->F > 0) {  // fixedI shuffled before markerI (BayesRv2Groups.cpp:216,227)
+        s->grand.shuffle(s->ref_forder);
+        HIPCHK(hipMemcpyAsync(d.forder, s->ref_forder.data(), (size_t)s->F * 4, hipMemcpyHostToDevice, s->st));
+      }
+      s->grand.shuffle(s->ref_order);
+      if (int rc = upload_order(s, shard_visit(s))) return rc;
+      HIPCHK(launch_gram(d, 0, d.gram, nullptr, s->st));
+      HIPCHK(launch_gram(d, 1, d.xgram, d.xgramT, s->st));
+    } else {
+      HIPCHK(launch_perm(d, it, s->shard, true, s->st));
     }
-    s->grand.shuffle(s->ref_order);
-    if (int rc = upload_order(s, shard_visit(s))) return rc;
-    HIPCHK(launch_gram(d, 0, d.gram, nullptr, s->st));
-    HIPCHK(launch_gram(d, 1, d.xgram, d.xgramT, s->st));
-  } else {
-    HIPCHK(launch_perm(d, it, s->shard, true, s->st));
+    if (s->model == MODEL_GROUPS && s->F > 0)
+      HIPCHK(launch_fixed(d, it, s->order_mode == BRR_ORDER_BLOCKED, s->st));
+    if (sharded)
+      if (int rc = rows_flagged(s, H_ROW_SNAPSHOT)) return rc;
+    // epoch bases of the hand-over counters (cumulative over the session; fixed for the sweep's
+    // segments, whose block positions continue the sweep's)
+    d.sbase = s->sbase;
+    for (int k = 0; k < NPAR; ++k) d.gbase[k] = s->gbase[k];
+    s->sbase += s->nb;
+    for (int k = 0; k < NPAR; ++k) s->gbase[k] += (s->nb + NPAR - 1 - k) / NPAR;  // blocks s with s % NPAR == k
+    // per-marker constants of the sweep in visit order (every segment's positions)
+    HIPCHK(launch_prep(d, it, s->st));
   }
-  if (s->model == MODEL_GROUPS && s->F > 0)
-    HIPCHK(launch_fixed(d, it, s->order_mode == BRR_ORDER_BLOCKED, s->st));
-  if (sharded)
-    if (int rc = rows_flagged(s, H_ROW_SNAPSHOT)) return rc;
-  // epoch bases of the hand-over counters (cumulative over the session)
-  d.sbase = s->sbase;
-  for (int k = 0; k < NPAR; ++k) d.gbase[k] = s->gbase[k];
-  d.abase = s->abase;
-  if (s->fused.nsg > 0) s->abase += s->fused.nsg + 1 + s->fused.nred;
-  s->sbase += s->nb;
-  for (int k = 0; k < NPAR; ++k) s->gbase[k] += (s->nb + NPAR - 1 - k) / NPAR;  // blocks s with s % NPAR == k
-  // per-marker constants of the sweep in visit order
-  HIPCHK(launch_prep(d, it, s->st));
+  // this launch's block positions (the whole sweep, or exchange segment seg)
+  int s0 = 0, s1 = s->nb;
+  seg_range(s->nb, s->seg, s->nex, &s0, &s1);
+  d.seg0 = s0;
+  d.seg1 = s1;
   // the hot loop (lag-1 pipeline).  Fused: ONE persistent launch, workgroup 0 solves block s
   // while the streaming workgroups form block s+1's dots (device counters hand over).
   // Per-block fallback: stream(0), stream(1), solve(0), stream(2), solve(1), ... on the one
   // queue (every dependency ahead in queue order, the same device protocol never waits).
   double *ebuf[2] = {d.eps, d.eps2};
   const bool fused = s->fused.nsg > 0;
-  if (fused) {
+  if (s1 > s0 && fused) {
+    d.abase = s->abase;  // residency census epoch of this launch
+    s->abase += s->fused.nsg + 1 + s->fused.nred;
     Dev dp = d;
     dp.NG = s->fused.ngroups;
     dp.gtarget = s->fused.ngroups;
@@ -351,10 +368,11 @@ int do_sweep_local(brr_session *s) {
     } else {
       HIPCHK(launch_sweep_fused(dp, it, s->fused, s->st));
     }
-  } else {
+  } else if (s1 > s0) {
+    // eps buffers relative to the segment start: k_stream(b) reads ebuf[(b - s0) & 1]
     auto stream_b = [&](int b) -> int {
-      const double *ein = ebuf[b & 1];
-      double *eout = ebuf[(b + 1) & 1];
+      const double *ein = ebuf[(b - s0) & 1];
+      double *eout = ebuf[(b - s0 + 1) & 1];
       if (s->timing) {
         const size_t i0 = s->ev_used;
         hipEvent_t e0 = s->ev(), e1 = s->ev();
@@ -380,17 +398,18 @@ int do_sweep_local(brr_session *s) {
       }
       return 0;
     };
-    for (int b = 0; b < s->nb; ++b) {
+    for (int b = s0; b < s1; ++b) {
       if (int rc = stream_b(b)) return rc;
-      if (b >= 1)
+      if (b >= s0 + 1)
         if (int rc = solve_b(b - 1)) return rc;
     }
-    if (int rc = solve_b(s->nb - 1)) return rc;
+    if (int rc = solve_b(s1 - 1)) return rc;
   }
-  // E_{nb-2} (written by the last k_stream) minus the changes of the last two blocks; the
+  // E_{s1-2} (written by the last k_stream) minus the changes of the last two blocks; the
   // fused sweep has already applied them and written eps
-  const double *elast = fused ? d.eps : ebuf[s->nb & 1];
-  const int sa = (!fused && s->nb >= 2) ? (s->nb - 2) % NSLOT : -1, sb = fused ? -1 : (s->nb - 1) % NSLOT;
+  const int ns = s1 - s0;
+  const double *elast = (fused || ns == 0) ? d.eps : ebuf[ns & 1];
+  const int sa = (!fused && ns >= 2) ? (s1 - 2) % NSLOT : -1, sb = (fused || ns == 0) ? -1 : (s1 - 1) % NSLOT;
   if (sharded) {
     if (!s->ex_eps || !s->ex_stats) { set_error("exchange buffers not set"); return -1; }
     Dev dx = d;
@@ -399,16 +418,28 @@ int do_sweep_local(brr_session *s) {
   } else {
     HIPCHK(launch_rows(d, H_ROW_PENDING | H_ROW_WRITE | H_ROW_REDUCE, nullptr, s->st, elast, sa, sb));
   }
-  const int mode = s->model == MODEL_HORSESHOE ? H_MR_HS : H_MR_BAYESR;
-  HIPCHK(launch_markers(d, mode, it, s->st));
-  if (sharded)
-    HIPCHK(hipMemcpyAsync(s->ex_stats, d.stats, sizeof(double) * s->NS, hipMemcpyDeviceToDevice, s->st));
+  if (last) {
+    const int mode = s->model == MODEL_HORSESHOE ? H_MR_HS : H_MR_BAYESR;
+    HIPCHK(launch_markers(d, mode, it, s->st));
+    if (sharded)
+      HIPCHK(hipMemcpyAsync(s->ex_stats, d.stats, sizeof(double) * s->NS, hipMemcpyDeviceToDevice, s->st));
+  } else {
+    // an earlier exchange segment: only the residual delta; the statistics follow the last
+    HIPCHK(hipMemsetAsync(s->ex_stats, 0, sizeof(double) * s->NS, s->st));
+  }
   return 0;
 }
 
 int do_sweep_finish(brr_session *s) {
   const uint32_t it = (uint32_t)s->iteration;
   const bool sharded = s->nshard > 1;
+  if (sharded && s->seg < s->nex - 1) {
+    // the next exchange segment starts from eps = eps_segment_start + sum of the shards' deltas
+    if (int rc = rows_flagged(s, H_ROW_EXCHANGE | H_ROW_WRITE | H_ROW_SNAPSHOT, s->ex_eps)) return rc;
+    s->seg++;
+    return 0;
+  }
+  s->seg = 0;
   if (sharded) {
     if (int rc = rows_flagged(s, H_ROW_EXCHANGE | H_ROW_WRITE | H_ROW_REDUCE, s->ex_eps)) return rc;
     HIPCHK(launch_hyper(s->d, it, s->ex_stats, s->st));
@@ -416,6 +447,8 @@ int do_sweep_finish(brr_session *s) {
     HIPCHK(launch_hyper(s->d, it, s->d.stats, s->st));
   }
   s->iteration++;
+  s->d.seg0 = 0;
+  s->d.seg1 = s->nb;
   if (s->timing) return collect_timing(s);
   return 0;
 }
@@ -724,6 +757,7 @@ void brr_options_default(brr_options *o) {
   o->order_mode = BRR_ORDER_BLOCKED;
   o->shard_count = 1;
   o->row_shard_count = 1;
+  o->exchanges_per_sweep = 1;
 }
 
 const char *brr_last_error(void) { return g_last_error.c_str(); }
@@ -737,14 +771,7 @@ int brr_device_count(void) {
 brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_total,
                                 int64_t col_offset, int32_t K, int32_t groups, int64_t F,
                                 const brr_options *opt_in) {
-  brr_options opt;
-  brr_options_default(&opt);
-  if (opt_in) {
-    // an ABI-1 caller's struct ends before the row-shard fields: keep their defaults
-    if (opt_in->abi_version >= 2) opt = *opt_in;
-    else std::memcpy(&opt, opt_in, offsetof(brr_options, row_shard_rank));
-    opt.abi_version = BRR_ABI_VERSION;
-  }
+  brr_options opt = brr::options_from_caller(opt_in);
   if (opt.row_shard_count < 1) opt.row_shard_count = 1;
   const bool rows = opt.row_shard_count > 1;
   const int64_t N_total = opt.N_total > 0 ? opt.N_total : N;
@@ -809,6 +836,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   s->K = K; s->G = groups; s->F = (int)F; s->B = B; s->model = model;
   s->order_mode = opt.order_mode;
   s->shard = opt.shard_rank; s->nshard = opt.shard_count;
+  s->nex = s->nshard > 1 ? std::max(1, opt.exchanges_per_sweep) : 1;
   s->rshard = rows ? opt.row_shard_rank : 0; s->nrshard = opt.row_shard_count;
   if (hipEventCreateWithFlags(&s->ev_x, hipEventDisableTiming) != hipSuccess) {
     set_error("cannot create an event on HIP device %d", s->device);
@@ -822,6 +850,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   d.Ntot = N_total; d.row_offset = rows ? opt.row_offset : 0;
   d.ld = (N + SROWS - 1) / SROWS * SROWS;  // every streaming row tile inside the allocation (zero rows)
   d.K = K; d.G = groups; d.F = (int)F; d.B = B; d.nb = s->nb; d.model = model;
+  d.seg0 = 0; d.seg1 = s->nb;  // block positions of a launch (exchange segments: a part)
   // streaming geometry: row tiles of SROWS rows (k_stream), NC = B/128 column chunks
   d.R = SROWS;
   d.RG = (int)((N + SROWS - 1) / SROWS);
@@ -1347,18 +1376,20 @@ int brr_session_sweep(brr_session *s, int32_t n) {
   }
   HIPCHK(hipSetDevice(s->device));
   for (int r = 0; r < n; ++r) {
-    if (int rc = do_sweep_local(s)) return rc;
-    if (s->nshard > 1) {
-      // the one exchange step of the column-sharded sweep: sum of residual deltas
-      // (N doubles) and of the marker statistics, in place, on the session stream
-      ncclResult_t r1 = ncclAllReduce(s->ex_eps, s->ex_eps, (size_t)s->N, ncclDouble, ncclSum, s->comm, s->st);
-      ncclResult_t r2 = ncclAllReduce(s->ex_stats, s->ex_stats, (size_t)s->NS, ncclDouble, ncclSum, s->comm, s->st);
-      if (r1 != ncclSuccess || r2 != ncclSuccess) {
-        set_error("ncclAllReduce failed: %s", ncclGetErrorString(r1 != ncclSuccess ? r1 : r2));
-        return -2;
+    for (int e = 0; e < s->nex; ++e) {
+      if (int rc = do_sweep_local(s)) return rc;
+      if (s->nshard > 1) {
+        // the exchange step of the column-sharded sweep (E per sweep): sum of residual
+        // deltas (N doubles) and of the marker statistics, in place, on the session stream
+        ncclResult_t r1 = ncclAllReduce(s->ex_eps, s->ex_eps, (size_t)s->N, ncclDouble, ncclSum, s->comm, s->st);
+        ncclResult_t r2 = ncclAllReduce(s->ex_stats, s->ex_stats, (size_t)s->NS, ncclDouble, ncclSum, s->comm, s->st);
+        if (r1 != ncclSuccess || r2 != ncclSuccess) {
+          set_error("ncclAllReduce failed: %s", ncclGetErrorString(r1 != ncclSuccess ? r1 : r2));
+          return -2;
+        }
       }
+      if (int rc = do_sweep_finish(s)) return rc;
     }
-    if (int rc = do_sweep_finish(s)) return rc;
   }
   return check_device_error(s);
 }
@@ -1457,6 +1488,8 @@ int brr_session_sweep_finish(brr_session *s) {
   HIPCHK(hipSetDevice(s->device));
   return do_sweep_finish(s);
 }
+
+int32_t brr_session_exchanges_per_sweep(brr_session *s) { return s ? s->nex : -1; }
 
 int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
   if (!s || !out) return -1;
@@ -1714,6 +1747,19 @@ int brr_session_synchronize(brr_session *s) {
 // ---------------------------------------------------------------------------------------
 // Sample output ring (brr_sample.hpp)
 namespace brr {
+
+brr_options options_from_caller(const brr_options *in) {
+  brr_options o;
+  brr_options_default(&o);
+  if (in) {
+    if (in->abi_version >= 3) o = *in;
+    else if (in->abi_version == 2) std::memcpy(&o, in, offsetof(brr_options, exchanges_per_sweep));
+    else std::memcpy(&o, in, offsetof(brr_options, row_shard_rank));
+    o.abi_version = BRR_ABI_VERSION;
+  }
+  if (o.exchanges_per_sweep < 1) o.exchanges_per_sweep = 1;
+  return o;
+}
 
 int sample_ring_open(brr_session *s, int depth) {
   sample_ring_close(s);

@@ -1,6 +1,7 @@
 """Column-sharded multi-GPU driver helpers: one process per GPU, markers split
 into contiguous ranges of whole blocks, the residual kept coherent by ONE all-reduce of the
-residual deltas (and the marker statistics) per sweep.
+residual deltas (and the marker statistics) per sweep -- or per exchange segment, with
+brr_options.exchanges_per_sweep = E > 1 (E rounds per sweep).
 
 Two exchange paths share the same session protocol (brr_session_sweep_local -> sum ->
 brr_session_sweep_finish):
@@ -39,8 +40,10 @@ class HostExchange:
         self.dist = dist
 
     def sweep(self, shard, n: int = 1):
+        """n sweeps; a sweep is `shard.exchanges_per_sweep` local / all-reduce / finish rounds."""
         import torch
-        for _ in range(n):
+        rounds = getattr(shard, "exchanges_per_sweep", 1)
+        for _ in range(n * rounds):
             shard.sweep_local()
             e, s = shard.exchange_get()
             te, ts = torch.from_numpy(e), torch.from_numpy(s)

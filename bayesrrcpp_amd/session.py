@@ -29,14 +29,15 @@ class Session:
     def __init__(self, model, N, M, *, K=1, groups=1, F=0, M_total=None, col_offset=0,
                  device=0, block_size=0, order_mode=L.ORDER_BLOCKED, shard_rank=0,
                  shard_count=1, verbose=0, log=None, x_storage=L.X_F32, row_shard_rank=0,
-                 row_shard_count=1, row_offset=0, N_total=0):
+                 row_shard_count=1, row_offset=0, N_total=0, exchanges_per_sweep=1):
         self._keep = []
         self.model, self.N, self.M, self.K, self.G, self.F = model, N, M, K, groups, F
         self.M_total = M if M_total is None else M_total
         self.col_offset = col_offset
         self.row_offset, self.N_total = row_offset, (N_total or N)
         self.opt = L.options(device, block_size, order_mode, shard_rank, shard_count, verbose, log,
-                             x_storage, row_shard_rank, row_shard_count, row_offset, N_total)
+                             x_storage, row_shard_rank, row_shard_count, row_offset, N_total,
+                             exchanges_per_sweep)
         self.h = L.lib().brr_session_create(model, N, M, self.M_total, col_offset, K, groups, F,
                                             C.byref(self.opt))
         if not self.h:
@@ -172,6 +173,11 @@ class Session:
 
     def sweep_finish(self):
         L.check(L.lib().brr_session_sweep_finish(self.h), "sweep_finish")
+
+    @property
+    def exchanges_per_sweep(self):
+        """local / exchange / finish rounds per sweep (column shards, brr_options.exchanges_per_sweep)"""
+        return L.lib().brr_session_exchanges_per_sweep(self.h)
 
     def synchronize(self):
         L.check(L.lib().brr_session_synchronize(self.h), "synchronize")

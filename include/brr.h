@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define BRR_ABI_VERSION 2
+#define BRR_ABI_VERSION 3
 
 enum brr_model { BRR_MODEL_V2 = 0, BRR_MODEL_GROUPS = 1, BRR_MODEL_RESTART = 2, BRR_MODEL_HORSESHOE = 3 };
 
@@ -81,6 +81,12 @@ typedef struct brr_options {
   int32_t row_shard_count; /* default 1 (no row sharding) */
   int64_t row_offset;      /* first global row of this shard */
   int64_t N_total;         /* rows of the whole cohort (0 = N) */
+  /* column shards (ABI 3): residual exchanges per sweep E (default 1 = once per sweep, SURVEY
+   * 8e).  Each shard's block positions split into E segments of whole blocks (segment e = blocks
+   * [nb e / E, nb (e + 1) / E)); after every segment the residual deltas are summed across the
+   * shards, so a shard sees the other shards' changes at most one segment late instead of one
+   * sweep (smaller stale-residual bias).  Ignored without column shards. */
+  int32_t exchanges_per_sweep;
 } brr_options;
 
 void brr_options_default(brr_options *opt);
@@ -172,6 +178,10 @@ int brr_session_sweep(brr_session *s, int32_t n);
  *   caller all-reduces (sum) the exchange buffers across processes (RCCL / gloo);
  *   brr_session_sweep_finish(s) -> eps = eps_start + sum dEps, hyper-parameter draws
  *                                  (redundant and identical on every process).
+ * With exchanges_per_sweep = E > 1 a sweep is E such rounds: local covers one segment of the
+ * shard's blocks (mu and fixed effects in the first only, the statistics in the last only --
+ * zeros before), finish sets eps = eps_segment_start + sum dEps and, after the last segment, draws
+ * the hyper-parameters.  brr_session_exchanges_per_sweep() returns E.
  * Exchange buffers are device memory owned by the caller (e.g. torch tensors), sizes from
  * brr_session_exchange_sizes(). */
 int brr_session_exchange_sizes(brr_session *s, int64_t *n_eps, int64_t *n_stats);
@@ -182,6 +192,7 @@ int brr_session_exchange_buffers(brr_session *s, double **dev_eps, double **dev_
 int brr_session_exchange_copy(brr_session *s, int32_t dir, double *host_eps, double *host_stats);
 int brr_session_sweep_local(brr_session *s);
 int brr_session_sweep_finish(brr_session *s);
+int32_t brr_session_exchanges_per_sweep(brr_session *s);
 /* the same split for init, needed by the restart model only (its pi init counts every
  * marker's component, src/BRv2Grstart.cpp:157-165): brr_session_init_local(s, seed) leaves
  * this shard's counts in the exchange statistics; the caller sums them across shards (as for a

@@ -504,6 +504,7 @@ struct orc {
   double *stats;      /* [sum b^2, sum b^2/lambda, betaAcum[G], v[G*K]] used by the epilogue */
   double *deps;       /* shard_only: this shard's eps - eps_start */
   orc_rstream *rs;    /* r_compat stream (orc_set_rng_r), NULL = Philox */
+  int seg;            /* shard_only: the exchange segment of the current sweep (n_exchanges) */
 };
 
 static double *dalloc(int64_t n) { return (double *)calloc((size_t)(n > 0 ? n : 1), sizeof(double)); }
@@ -521,6 +522,7 @@ orc *orc_create(const orc_config *cfg) {
   o->F = cfg->model == ORC_GROUPS ? cfg->F : 0;
   if (o->c.n_shards < 1) o->c.n_shards = 1;
   if (o->c.shard_only >= o->c.n_shards) o->c.shard_only = -1;
+  if (o->c.n_exchanges < 1 || o->c.n_shards <= 1) o->c.n_exchanges = 1;
   if (o->c.block_size < 1) o->c.block_size = 256;
   o->seed = (uint64_t)(int64_t)cfg->seed;
   o->eps = dalloc(o->N);
@@ -826,18 +828,24 @@ static void fixed_effects(orc *o) {
   }
 }
 
-static void marker_pass(orc *o) {
+/* positions [*p0, *p1) of a shard's ps visit positions that form exchange segment e: whole
+ * blocks of B positions, blocks [nbl e / E, nbl (e + 1) / E) of the shard's nbl blocks (the
+ * device splits a shard's block positions the same way, brr_session.cpp seg_range) */
+static void seg_positions(const orc *o, int64_t ps, int e, int64_t *p0, int64_t *p1) {
+  const int64_t B = o->c.block_size, E = o->c.n_exchanges;
+  const int64_t nbl = (ps + B - 1) / B;
+  const int64_t b0 = nbl * e / E, b1 = nbl * (e + 1) / E;
+  *p0 = b0 * B < ps ? b0 * B : ps;
+  *p1 = b1 * B < ps ? b1 * B : ps;
+}
+
+/* column-sharded protocol for exchange segment e: every shard sweeps its segment's
+ * positions against its own copy of epsilon from the segment start; then
+ * eps = eps_start + sum_s (eps_s - eps_start).  shard_only >= 0: this process's shard only, the
+ * delta left in deps for the caller's all-reduce. */
+static void marker_segment(orc *o, int e) {
   const int64_t N = o->N;
   const int hs = o->c.model == ORC_HORSESHOE;
-  if (o->c.n_shards <= 1) {
-    for (int64_t j = 0; j < o->P; ++j) {
-      int64_t m = o->order[j];
-      if (hs) horseshoe_marker(o, m, o->eps); else bayesr_marker(o, m, o->eps);
-    }
-    return;
-  }
-  /* column-sharded protocol: every shard sweeps its columns against its own
-   * copy of epsilon; eps = eps_start + sum_s (eps_s - eps_start). */
   memcpy(o->eps_start, o->eps, sizeof(double) * (size_t)N);
   memset(o->eps_acc, 0, sizeof(double) * (size_t)N);
   int64_t pos = 0;
@@ -847,7 +855,9 @@ static void marker_pass(orc *o) {
     int64_t ps = shard_range(o, s, &off);
     if (o->c.shard_only >= 0 && s != o->c.shard_only) { pos += ps; continue; }
     memcpy(o->eps, o->eps_start, sizeof(double) * (size_t)N);
-    for (int64_t j = 0; j < ps; ++j) {
+    int64_t j0, j1;
+    seg_positions(o, ps, e, &j0, &j1);
+    for (int64_t j = j0; j < j1; ++j) {
       int64_t m = ord[pos + j];
       if (hs) horseshoe_marker(o, m, o->eps); else bayesr_marker(o, m, o->eps);
     }
@@ -860,6 +870,25 @@ static void marker_pass(orc *o) {
   }
   for (int64_t i = 0; i < N; ++i) o->eps[i] = o->eps_start[i] + o->eps_acc[i];
 }
+
+static void marker_pass(orc *o) {
+  const int hs = o->c.model == ORC_HORSESHOE;
+  if (o->c.n_shards <= 1) {
+    for (int64_t j = 0; j < o->P; ++j) {
+      int64_t m = o->order[j];
+      if (hs) horseshoe_marker(o, m, o->eps); else bayesr_marker(o, m, o->eps);
+    }
+    return;
+  }
+  if (o->c.shard_only >= 0) {
+    marker_segment(o, o->seg);
+    return;
+  }
+  for (int e = 0; e < o->c.n_exchanges; ++e) marker_segment(o, e);
+}
+
+/* shard_only: this sweep's last exchange segment (the statistics and the epilogue follow it) */
+static int last_seg(const orc *o) { return o->c.shard_only < 0 || o->seg == o->c.n_exchanges - 1; }
 
 /* statistics the epilogue needs, over this process's markers (all markers unless shard_only) */
 static void compute_stats(orc *o) {
@@ -887,12 +916,18 @@ static void bayesr_epilogue(orc *o);
 static void sweep_bayesr(orc *o) {
   const int K = o->K, G = o->G;
   const orc_config *c = &o->c;
-  mu_update(o);
-  make_orders(o);
-  if (c->model == ORC_GROUPS) fixed_effects(o);
-  memset(o->v, 0, sizeof(double) * (size_t)(G * K));
-  memset(o->betaAcum, 0, sizeof(double) * (size_t)G);
+  if (o->seg == 0) {
+    mu_update(o);
+    make_orders(o);
+    if (c->model == ORC_GROUPS) fixed_effects(o);
+    memset(o->v, 0, sizeof(double) * (size_t)(G * K));
+    memset(o->betaAcum, 0, sizeof(double) * (size_t)G);
+  }
   marker_pass(o);
+  if (!last_seg(o)) {  /* an earlier exchange segment: nothing but the residual delta */
+    memset(o->stats, 0, sizeof(double) * (size_t)orc_stats_size(o));
+    return;
+  }
   compute_stats(o);
   if (c->model != ORC_HORSESHOE && o->c.shard_only >= 0) return; /* epilogue after exchange */
   bayesr_epilogue(o);
@@ -951,15 +986,21 @@ static void sweep_horseshoe(orc *o) {
   const int64_t P = o->P;
   const uint32_t it = (uint32_t)o->it;
   const orc_config *c = &o->c;
-  mu_update(o);
-  make_orders(o);
-  o->eta = inv_gamma_rate_rng(o->seed, 0.5 + 0.5 * c->vT,
-                              (1.0 / (o->sigmaE * c->A * c->A)) + c->vT / o->tau,
-                              ORC_T_HS_ETA, 0, it);                                 /* :217 */
-  for (int64_t j = 0; j < P; ++j)                                                   /* :218 */
-    o->hsv[j] = inv_gamma_rate_rng(o->seed, 0.5 + 0.5 * c->vL, c->vL / o->lambda[j] + 1.0,
-                                   ORC_T_HS_V, (uint32_t)j, it);
+  if (o->seg == 0) {
+    mu_update(o);
+    make_orders(o);
+    o->eta = inv_gamma_rate_rng(o->seed, 0.5 + 0.5 * c->vT,
+                                (1.0 / (o->sigmaE * c->A * c->A)) + c->vT / o->tau,
+                                ORC_T_HS_ETA, 0, it);                               /* :217 */
+    for (int64_t j = 0; j < P; ++j)                                                 /* :218 */
+      o->hsv[j] = inv_gamma_rate_rng(o->seed, 0.5 + 0.5 * c->vL, c->vL / o->lambda[j] + 1.0,
+                                     ORC_T_HS_V, (uint32_t)j, it);
+  }
   marker_pass(o);                                                                   /* :219-240 */
+  if (!last_seg(o)) {
+    memset(o->stats, 0, sizeof(double) * (size_t)orc_stats_size(o));
+    return;
+  }
   int64_t j0 = 0, j1 = P;
   if (o->c.shard_only >= 0) j1 = j0 + shard_range(o, o->c.shard_only, &j0);
   for (int64_t j = j0; j < j1; ++j)                                                 /* :242 */
@@ -1010,6 +1051,11 @@ int orc_exchange_set(orc *o, const double *deps_sum, const double *stats_sum) {
 }
 
 int orc_sweep_finish(orc *o) {
+  if (o->c.shard_only >= 0 && o->seg < o->c.n_exchanges - 1) {  /* the next exchange segment */
+    o->seg++;
+    return 0;
+  }
+  o->seg = 0;
   g_rs = o->rs;
   if (o->c.model == ORC_HORSESHOE) hs_epilogue(o); else bayesr_epilogue(o);
   g_rs = NULL;

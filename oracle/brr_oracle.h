@@ -75,6 +75,12 @@ typedef struct orc_config {
   const double *pi0;          /* optional G x K (row-major per group) initial pi override */
   int32_t shard_only;         /* -1: emulate all n_shards in-process; s >= 0: this process
                                  sweeps shard s only and exchanges through orc_exchange_* */
+  int32_t n_exchanges;        /* column shards: residual exchanges per sweep E (< 1 = 1).  Each
+                                 shard's visit positions split into E segments of whole blocks
+                                 (segment e = blocks [nb e / E, nb (e + 1) / E) of the shard);
+                                 after every segment eps = eps_seg_start + sum of the shards'
+                                 deltas.  With shard_only >= 0 every segment is one
+                                 orc_sweep_local / orc_exchange_* / orc_sweep_finish round. */
 } orc_config;
 
 typedef struct orc orc;

@@ -44,7 +44,7 @@ class OrcConfig(C.Structure):
         ("eps0", C.POINTER(C.c_double)), ("comp0", C.POINTER(C.c_double)),
         ("seed", C.c_int32), ("order_mode", C.c_int32), ("block_size", C.c_int32),
         ("n_shards", C.c_int32), ("pi0", C.POINTER(C.c_double)),
-        ("shard_only", C.c_int32),
+        ("shard_only", C.c_int32), ("n_exchanges", C.c_int32),
     ]
 
 
@@ -189,7 +189,7 @@ class Oracle:
                  sigma0=0.01, v0E=1e-4, s02E=1e-3, v0G=1e-4, s02G=1e-3,
                  A=1.0, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0,
                  mu0=0.0, sigmaE0=1.0, beta0=None, sigmaGG0=None, eps0=None, comp0=None,
-                 pi0=None, N=None, shard_only=-1, r_seed=None):
+                 pi0=None, N=None, shard_only=-1, r_seed=None, n_exchanges=1):
         # r_seed: draw from the r_compat stream (R's set.seed(r_seed) Mersenne-Twister /
         # Inversion / rgamma / rbeta, in the reference's call order) instead of Philox
         self._keep = []
@@ -232,6 +232,7 @@ class Oracle:
         cfg.block_size = block_size or (128 if model in (HORSESHOE, GROUPS) or N < 32768 else 512)
         cfg.n_shards = n_shards
         cfg.shard_only = shard_only
+        cfg.n_exchanges = n_exchanges
         self.cfg = cfg
         self.N, self.P, self.K, self.G = N, P, cfg.K, G
         self.h = lib().orc_create(C.byref(cfg))
@@ -244,6 +245,11 @@ class Oracle:
     def sweep(self, n=1):
         lib().orc_sweep(self.h, n)
         return self
+
+    @property
+    def exchanges_per_sweep(self):
+        """per-shard protocol: local / exchange / finish rounds per sweep (n_exchanges)"""
+        return self.cfg.n_exchanges if self.cfg.n_shards > 1 and self.cfg.shard_only >= 0 else 1
 
     # per-shard protocol (shard_only >= 0): local sweep -> exchange -> finish
     def sweep_local(self):

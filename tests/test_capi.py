@@ -85,11 +85,13 @@ def test_header_compiles_as_c(tmp_path):
 
 
 def test_options_struct_layout(brr, tmp_path):
-    # the ctypes mirror has the C compiler's layout of brr_options (ABI 2: row-shard fields)
+    # the ctypes mirror has the C compiler's layout of brr_options (ABI 2: row-shard fields, ABI 3:
+    # exchanges_per_sweep)
     from bayesrrcpp_amd import _lib
     o = _lib.options()
-    assert o.abi_version == _lib.ABI_VERSION == 2
+    assert o.abi_version == _lib.ABI_VERSION == 3
     assert o.row_shard_count == 1 and o.row_shard_rank == 0 and o.N_total == 0
+    assert o.exchanges_per_sweep == 1
     src = tmp_path / "lay.c"
     fields = [f[0] for f in _lib.Options._fields_]
     src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "brr.h"\nint main(void){'

@@ -1,6 +1,7 @@
 """Multi-process (gloo, world_size 2) test of the column-sharded exchange protocol on CPU:
 two processes, each sweeping its own shard and summing the residual deltas + statistics with
-torch.distributed, reproduce the single-process 2-shard emulation bit for bit.  The GPU path
+torch.distributed, reproduce the single-process 2-shard emulation bit for bit -- also with E
+residual exchanges per sweep (brr_options.exchanges_per_sweep).  The GPU path
 runs the same protocol with ncclAllReduce inside libbrr (tests/test_gpu_parity.py covers the
 device side on one GPU)."""
 import os
@@ -20,7 +21,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, model, out_dir, order=0):
+def _worker(rank, world, port, model, out_dir, order=0, E=1):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -31,7 +32,8 @@ def _worker(rank, world, port, model, out_dir, order=0):
     X, Y, _ = O.synth_cohort(11, 240, 384, n_causal=20)
     kw = dict(cva=CVA, **HYP) if model == O.V2 else dict(A=0.01, v0E=1e-3, s02E=1e-3, vL=1, vT=1,
                                                         c2=1, vC=10, sC=10)
-    o = O.Oracle(model, X, Y, seed=3, block_size=64, n_shards=world, shard_only=rank, order_mode=order, **kw)
+    o = O.Oracle(model, X, Y, seed=3, block_size=64, n_shards=world, shard_only=rank, order_mode=order,
+                 n_exchanges=E, **kw)
     HostExchange(dist).sweep(o, 3)
     np.save(os.path.join(out_dir, f"beta{rank}.npy"), o.vector(O.V_BETA))
     np.save(os.path.join(out_dir, f"eps{rank}.npy"), o.vector(O.V_EPS))
@@ -41,16 +43,17 @@ def _worker(rank, world, port, model, out_dir, order=0):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("model,order", [(0, 0), (3, 0), (0, 1), (3, 1)])  # BLOCKED, REFERENCE
-def test_gloo_two_ranks_match_emulation(oracle_mod, tmp_path, model, order):
+@pytest.mark.parametrize("model,order,E", [(0, 0, 1), (3, 0, 1), (0, 1, 1), (3, 1, 1),  # BLOCKED, REFERENCE
+                                           (0, 0, 2), (3, 0, 3), (0, 1, 3)])  # E exchanges per sweep
+def test_gloo_two_ranks_match_emulation(oracle_mod, tmp_path, model, order, E):
     import torch.multiprocessing as mp
     O = oracle_mod
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), model, str(tmp_path), order), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), model, str(tmp_path), order, E), nprocs=world, join=True)
     X, Y, _ = O.synth_cohort(11, 240, 384, n_causal=20)
     kw = dict(cva=CVA, **HYP) if model == O.V2 else dict(A=0.01, v0E=1e-3, s02E=1e-3, vL=1, vT=1,
                                                         c2=1, vC=10, sC=10)
-    ref = O.Oracle(model, X, Y, seed=3, block_size=64, n_shards=world, order_mode=order, **kw)
+    ref = O.Oracle(model, X, Y, seed=3, block_size=64, n_shards=world, order_mode=order, n_exchanges=E, **kw)
     ref.sweep(3)
     from bayesrrcpp_amd.distributed import shard_columns
     beta = np.zeros(384)
