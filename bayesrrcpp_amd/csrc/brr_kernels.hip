@@ -2744,11 +2744,11 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
 #else
 #define BRR_SOLVER_INL __forceinline__
 #endif
-template <bool HS, int B>
+template <bool HS, int B, int NT = SWEEP_NT>
 __device__ BRR_SOLVER_INL void solver_role(const Dev &d, uint32_t it, int nslot, char *smem) {
   int gi_pref = 0;
   for (int s = d.seg0; s < d.seg1; ++s) {
-    solve_block<HS, B, SWEEP_NT>(d, s, it, nslot, smem, true, gi_pref);
+    solve_block<HS, B, NT>(d, s, it, nslot, smem, true, gi_pref);
     __syncthreads();
   }
 }
@@ -2791,6 +2791,53 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
   }
 }
 
+
+// The same marker loop as two kernels launched side by side (the default): the solver workgroup in
+// k_sweep_solve, the streaming and reducing workgroups in k_sweep_stream.  Each gets its own
+// register allocation (in k_sweep every role shares the largest role's, and the solver's serial
+// chain reloads spilled registers from scratch memory).  Residency: the solver needs a whole CU's
+// LDS and every streaming / reducing workgroup is padded to more than half of it, so no two
+// workgroups of this launch pair share a CU and 1 + nsg + nred <= #CUs of them are resident at
+// once; the census below (across both kernels) is the defence, as in k_sweep.
+__device__ __forceinline__ bool sweep_census(const Dev &d, int total, int *s_ok) {
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(d.sync + SY_ARRIVE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    wait_geq(d.sync + SY_ARRIVE, d.abase + total, d.sync, 5);
+    *s_ok = ld_sc1_int(d.sync + SY_ERR) == 0;
+  }
+  __syncthreads();
+  return *s_ok != 0;
+}
+
+constexpr int SOLVE_NT = SWEEP_NT;  // the solver workgroup's threads
+template <bool HS, int B>
+__global__ __launch_bounds__(SOLVE_NT, 1) void k_sweep_solve(Dev d, uint32_t it, int nslot, int total) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int s_ok;
+  if (!sweep_census(d, total, &s_ok)) return;
+  solver_role<HS, B, SOLVE_NT>(d, it, nslot, smem);
+}
+
+template <int XF>
+__global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep_stream(Dev d, int nsg, int rpw, int npass, int nred, int ccache) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int s_np[2];
+  __shared__ int s_ok;
+  if (!sweep_census(d, nsg + 1 + nred, &s_ok)) return;
+  if ((int)blockIdx.x >= nsg) {
+    reduce_role(d, (int)blockIdx.x - nsg, nsg, nred, d.sc->prof_on);
+    return;
+  }
+  double *eps_l = reinterpret_cast<double *>(smem);
+  double *s_lut = eps_l + (int64_t)npass * SROWS;
+  double *s_pbo = s_lut + (XF ? (int64_t)(d.lag + 3) * d.B * 4 : 0), *s_pbn = s_pbo + (d.B + 16);
+  int *s_pidx = reinterpret_cast<int *>(s_pbn + (d.B + 16));
+  int *s_mem = s_pidx + (d.B + 16);
+  double *s_part = reinterpret_cast<double *>(s_mem + 2 * d.B);
+  uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_part + SWEEP_NW * SROWS) : nullptr;
+  stream_role<STREAM_CW, XF ? STREAM_P2 : STREAM_P, XF>(d, (int)blockIdx.x, rpw, npass, eps_l, s_pidx, s_pbo, s_pbn,
+                                                       s_np, s_lut, s_mem, s_part, s_codes);
+}
 
 // ------------------------------------------------------------------------------------
 // Marker pass: Horseshoe v / lambda draws (HorseshoeR.cpp:218,242) and the statistics the
@@ -3115,6 +3162,24 @@ static const void *sweep_kernel(int model, int B, bool xf) {
   }
 }
 
+template <bool HS, int B>
+static const void *solve_fn() { return (const void *)k_sweep_solve<HS, B>; }
+
+static const void *solve_kernel(int model, int B) {
+  const bool hs = model == MODEL_HORSESHOE;
+  switch (B) {
+    case 128: return hs ? solve_fn<true, 128>() : solve_fn<false, 128>();
+    case 256: return hs ? solve_fn<true, 256>() : solve_fn<false, 256>();
+    case 512: return hs ? solve_fn<true, 512>() : solve_fn<false, 512>();
+    default: return nullptr;
+  }
+}
+
+static const void *stream_kernel(bool xf) { return xf ? (const void *)k_sweep_stream<1> : (const void *)k_sweep_stream<0>; }
+
+// streaming / reducing workgroups of the two-kernel sweep take more than half of a CU's LDS: one per CU
+constexpr size_t STREAM_LDS_MIN = SOLVE_LDS_MAX / 2 + 1024;
+
 bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   // the 8 waves of a streaming workgroup split a block's columns in chunks of STREAM_CW
   if (cus < 3 || d.B % (SWEEP_NW * STREAM_CW) != 0) return false;
@@ -3136,29 +3201,48 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   const int nred = ngr(nsg);
   if (nsg > d.RG + 1) return false;  // slab1 rows
   const bool xf = d.Xc != nullptr;
-  const void *fn = sweep_kernel(d.model, d.B, xf);
+  // BRR_FUSED_SINGLE=1: every role in the one cooperative k_sweep launch (the round-2 form)
+  const char *one = getenv("BRR_FUSED_SINGLE");
+  const bool split = !(one && one[0] == '1');
+  const void *fn = split ? solve_kernel(d.model, d.B) : sweep_kernel(d.model, d.B, xf);
+  const void *fst = split ? stream_kernel(xf) : nullptr;
   if (!fn) return false;
-  hipFuncAttributes attr;
+  hipFuncAttributes attr, attr_st;
   if (hipFuncGetAttributes(&attr, fn) != hipSuccess) return false;
+  if (split && hipFuncGetAttributes(&attr_st, fst) != hipSuccess) return false;
   const size_t budget = SOLVE_LDS_MAX - attr.sharedSizeBytes;
   const int K = d.model == MODEL_HORSESHOE ? 1 : d.K;
   const size_t fixed = solve_fixed_bytes(d.B, K);
   if (fixed + 8 * (size_t)d.B > budget) return false;
-  const int nslot = (int)std::min<size_t>((size_t)solve_max_slots(d.B, SWEEP_NT), (budget - fixed) / (8 * (size_t)d.B));
-  if ((size_t)nslot * d.B < solve_scratch_doubles(d.B, SWEEP_NT)) return false;
+  const int snt = split ? SOLVE_NT : SWEEP_NT;  // the solver workgroup's threads
+  const int nslot = (int)std::min<size_t>((size_t)solve_max_slots(d.B, snt), (budget - fixed) / (8 * (size_t)d.B));
+  if ((size_t)nslot * d.B < solve_scratch_doubles(d.B, snt)) return false;
   // streamers: residual rows, [the value tables of two blocks], the change list (indices, old and
   // new betas), the member indices of two blocks in LDS
   const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double) + (xf ? (size_t)d.B * 32 * (d.lag + 3) : 0) +
                            (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int)) + 2 * sizeof(int) * d.B +
                            (size_t)SWEEP_NW * SROWS * sizeof(double);
   const size_t code_bytes = xf ? (size_t)(d.lag + 2) * d.B * npass * 64 : 0;
-  const bool ccache = xf && eps_bytes + code_bytes <= budget && !getenv("BRR_NO_CODE_CACHE");
-  const size_t lds = std::max(fixed + (size_t)nslot * 8 * d.B, eps_bytes + (ccache ? code_bytes : 0));
-  if (lds > budget) return false;
+  const size_t st_budget = split ? SOLVE_LDS_MAX - attr_st.sharedSizeBytes : budget;
+  const bool ccache = xf && eps_bytes + code_bytes <= st_budget && !getenv("BRR_NO_CODE_CACHE");
+  const size_t st_lds = eps_bytes + (ccache ? code_bytes : 0);
+  const size_t lds = split ? fixed + (size_t)nslot * 8 * d.B : std::max(fixed + (size_t)nslot * 8 * d.B, st_lds);
+  if (lds > budget || st_lds > st_budget) return false;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) != hipSuccess) return false;
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, SWEEP_NT, lds) != hipSuccess || per_cu < 1)
+  if (split && hipFuncSetAttribute(fst, hipFuncAttributeMaxDynamicSharedMemorySize, (int)st_budget) != hipSuccess)
     return false;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, snt, lds) != hipSuccess || per_cu < 1)
+    return false;
+  cfg->split = split ? 1 : 0;
+  // (split) the streaming kernel's LDS request: padded past half a CU's LDS, one workgroup per CU
+  cfg->st_lds = split ? std::min(st_budget, std::max(st_lds, STREAM_LDS_MIN - attr_st.sharedSizeBytes)) : 0;
+  if (split) {
+    per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fst, SWEEP_NT, cfg->st_lds) != hipSuccess || per_cu != 1)
+      return false;
+    if (1 + nsg + nred > cus) return false;
+  }
   cfg->nsg = nsg;
   cfg->rpw = (int)rpw;
   cfg->npass = npass;
@@ -3173,12 +3257,30 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
 // A cooperative launch: the runtime starts the grid only when every workgroup can be resident
 // at once (or fails the launch), which the in-kernel hand-over relies on.  BRR_TEST_CENSUS_EXTRA
 // (tests) raises the census target above the grid to exercise the failed-census exit.
-hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipStream_t st) {
-  const void *fn = sweep_kernel(d.model, d.B, d.Xc != nullptr);
-  if (!fn) return hipErrorInvalidValue;
+hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipStream_t st, hipStream_t st_side,
+                              hipEvent_t ev_go, hipEvent_t ev_done) {
   Dev dd = d;
   if (const char *ex = getenv("BRR_TEST_CENSUS_EXTRA")) dd.abase += atoi(ex);
   int nslot = c.nslot, nsg = c.nsg, rpw = c.rpw, npass = c.npass, nred = c.nred, cc = c.ccache;
+  if (c.split) {
+    // the streaming kernel on the side stream, released by the same event that precedes the
+    // solver on the session stream; the session stream waits for it before the next launch
+    const void *fs = solve_kernel(d.model, d.B), *ft = stream_kernel(d.Xc != nullptr);
+    if (!fs || !ft) return hipErrorInvalidValue;
+    int total = nsg + 1 + nred;
+    hipError_t e = hipEventRecord(ev_go, st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st_side, ev_go, 0);
+    void *sargs[] = {&dd, &it, &nslot, &total};
+    if (e == hipSuccess) e = hipLaunchKernel(fs, dim3(1), dim3(SOLVE_NT), sargs, (unsigned)c.lds, st);
+    void *targs[] = {&dd, &nsg, &rpw, &npass, &nred, &cc};
+    if (e == hipSuccess)
+      e = hipLaunchKernel(ft, dim3((unsigned)(nsg + nred)), dim3(SWEEP_NT), targs, (unsigned)c.st_lds, st_side);
+    if (e == hipSuccess) e = hipEventRecord(ev_done, st_side);
+    if (e == hipSuccess) e = hipStreamWaitEvent(st, ev_done, 0);
+    return e;
+  }
+  const void *fn = sweep_kernel(d.model, d.B, d.Xc != nullptr);
+  if (!fn) return hipErrorInvalidValue;
   void *args[] = {&dd, &it, &nslot, &nsg, &rpw, &npass, &nred, &cc};
   // BRR_PLAIN_LAUNCH=1: a plain launch of the same kernel (the census then guards residency alone).
   // Used for rocprofv3 runs: with ROCm 7.2's rocprofv3 attached, a process that made a cooperative

@@ -136,6 +136,8 @@ struct brr_session {
   Dev d{};
   int device = 0;
   hipStream_t st = nullptr;
+  hipStream_t st_side = nullptr;  // two-kernel fused sweep: the streaming kernel's stream
+  hipEvent_t ev_go = nullptr, ev_done = nullptr;
   int sbase = 0, gbase[NPAR] = {}, abase = 0;  // hand-over counter epochs (see SyncWord)
   FusedCfg fused;       // fused persistent sweep (nsg == 0: per-block kernels)
   int64_t N = 0, M = 0, M_total = 0, col_offset = 0;
@@ -180,6 +182,10 @@ struct brr_session {
     for (void *p : allocs) (void)hipFree(p);
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
     if (ev_x) (void)hipEventDestroy(ev_x);
+    if (ev_go) (void)hipEventDestroy(ev_go);
+    if (ev_done) (void)hipEventDestroy(ev_done);
+    if (st_side) (void)hipStreamSynchronize(st_side);
+    if (st_side) (void)hipStreamDestroy(st_side);
     if (st) (void)hipStreamDestroy(st);
   }
   hipEvent_t ev() {
@@ -362,11 +368,11 @@ int do_sweep_local(brr_session *s) {
       const size_t i0 = s->ev_used;
       hipEvent_t e0 = s->ev(), e1 = s->ev();
       HIPCHK(hipEventRecord(e0, s->st));
-      HIPCHK(launch_sweep_fused(dp, it, s->fused, s->st));
+      HIPCHK(launch_sweep_fused(dp, it, s->fused, s->st, s->st_side, s->ev_go, s->ev_done));
       HIPCHK(hipEventRecord(e1, s->st));
       s->ev_pairs.push_back({i0, 3});
     } else {
-      HIPCHK(launch_sweep_fused(dp, it, s->fused, s->st));
+      HIPCHK(launch_sweep_fused(dp, it, s->fused, s->st, s->st_side, s->ev_go, s->ev_done));
     }
   } else if (s1 > s0) {
     // eps buffers relative to the segment start: k_stream(b) reads ebuf[(b - s0) & 1]
@@ -979,6 +985,14 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     if (rows || ref2bit || (pb && pb[0] == '1') || !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused))
       s->fused = FusedCfg{};
     if (s->fused.nsg == 0) d.lag = 1;
+    if (s->fused.split &&
+        (hipStreamCreateWithFlags(&s->st_side, hipStreamNonBlocking) != hipSuccess ||
+         hipEventCreateWithFlags(&s->ev_go, hipEventDisableTiming) != hipSuccess ||
+         hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming) != hipSuccess)) {
+      set_error("cannot create the streaming kernel's stream / events");
+      delete s;
+      return nullptr;
+    }
     if ((d.lag >= 2 && (s->alloc(&d.xgram2, (int64_t)s->nb * B * B) || s->alloc(&d.xgram2T, (int64_t)s->nb * B * B))) ||
         (d.lag >= 3 && (s->alloc(&d.xgram3, (int64_t)s->nb * B * B) || s->alloc(&d.xgram3T, (int64_t)s->nb * B * B)))) {
       delete s;

@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu ${TESTS:-tests/test_gpu_configs.py tests/test_gpu_rowshard.py} > gpurun_out/r3_tests.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu ${TESTS:-tests/test_gpu_exchange.py tests/test_gpu_configs.py tests/test_gpu_rowshard.py} > gpurun_out/r3_tests.log 2>&1; rc=$?
 tail -15 gpurun_out/r3_tests.log
 [ $rc -eq 0 ] || exit $rc
 for w in 4 8 20; do
