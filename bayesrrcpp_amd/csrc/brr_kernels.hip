@@ -1192,8 +1192,10 @@ __device__ __forceinline__ int reduce16_col(int lane) {
 //   slots    nslot Gram rows (B doubles each), staged for the positions predicted to change
 enum PrFlag : int { PF_EX = 1 << 8, PF_LIKELY = 1 << 9 };
 
-__host__ __device__ inline size_t solve_fixed_bytes(int B, int K) {
-  return (size_t)(10 + K + (K > 1 ? K - 1 : 0)) * 8 * B + (size_t)6 * 4 * B + 64;
+// nlb: change-list buffers kept in LDS from block to block (persistent solver: one per pipeline lag,
+// block s's list in buffer s % nlb, each B + 16 doubles of deltas and B + 16 Gram indices)
+__host__ __device__ inline size_t solve_fixed_bytes(int B, int K, int nlb = 0) {
+  return (size_t)(10 + K + (K > 1 ? K - 1 : 0)) * 8 * B + (size_t)6 * 4 * B + 128 + (size_t)nlb * 12 * (B + 16);
 }
 constexpr size_t SOLVE_LDS_MAX = 160 * 1024;
 // phase A scratch in the slot area (doubles): the change list (deltas, gram indices) and the
@@ -1551,7 +1553,13 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
          *Lx2 = Lbn + B, *Lp = Lx2 + B, *Lz = Lp + B, *La = Lz + B, *Lden = La + (int64_t)K * B;
   int *Lfl = reinterpret_cast<int *>(Lden + (int64_t)KD * B);
   int *Lks = Lfl + B, *Lgi = Lks + B, *Lm = Lgi + B, *Lslot = Lm + B, *Lspos = Lslot + B, *misc = Lspos + B;
-  double *slots = reinterpret_cast<double *>(misc + 16);
+  // persistent solver: the change lists of the last nlb blocks stay in LDS (buffer j: deltas at
+  // Llist + j (B + 16), Gram indices at Lligi + j (B + 16); misc[16 + 2 j] = padded length, misc[17 + 2 j]
+  // = its block), so the cross-Gram correction of the next blocks needs no round trip for them
+  const int nlb = persistent ? d.lag : 0;
+  double *Llist = reinterpret_cast<double *>(misc + 32);
+  int *Lligi = reinterpret_cast<int *>(Llist + (int64_t)nlb * (B + 16));
+  double *slots = reinterpret_cast<double *>(Lligi + (int64_t)nlb * (B + 16));
 
   const int t = threadIdx.x;
   const int lane = t & 63, wv = t >> 6;
@@ -1564,12 +1572,17 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   const int64_t S = d.nbB;
   const int64_t q0 = (int64_t)s * B;
   const bool resident = B <= RESIDENT_BMAX && nslot >= B + solve_scratch_rows(B, NT);
-  // misc[10] / misc[11]: padded length / block of the change list this workgroup left in LDS;
-  // misc[12]: block whose Gram copy into LDS the previous block already started
-  if (t == 0 && s == d.seg0) { misc[11] = -2; misc[12] = -2; }
+  // misc[12]: block whose Gram copy into LDS the previous block already started; misc[17 + 2 j]:
+  // block of the change list in LDS buffer j
+  if (t == 0 && s == d.seg0) {
+    misc[12] = -2;
+    for (int j = 0; j < LAG_MAX; ++j) misc[17 + 2 * j] = -2;
+  }
   const bool pipelined = persistent && resident;
-  const int gi_t = (pipelined && s > d.seg0) ? gi_pref : (t % B < bs ? d.gidx[q0 + t % B] : 0);
-  if (pipelined && s + 1 < d.seg1) gi_pref = d.gidx[(int64_t)(s + 1) * B + t % B];
+  // the Gram index of this thread's position, loaded one block ahead by the persistent solver
+  const bool prefgi = persistent && NPT == 1;
+  const int gi_t = (prefgi && s > d.seg0) ? gi_pref : (t % B < bs ? d.gidx[q0 + t % B] : 0);
+  if (prefgi && s + 1 < d.seg1) gi_pref = d.gidx[(int64_t)(s + 1) * B + t % B];
 
   // A) everything that does not depend on k_stream(s).  The per-position constants are loaded
   // first (vmcnt retires loads in order, so loads issued behind the 128 KiB Gram copy would wait
@@ -1618,86 +1631,110 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   // sum_i (x_j . x_i) delta_i over the changes of the blocks the streamed dots have not seen:
   // block s-1 (cross-Gram of cycle neighbours), and with lag 2 also block s-2 (cross-Gram of
   // blocks two apart), added in that order -- blocks of this launch only (seg0 onwards: the
-  // earlier ones' changes are in the residual the launch started from).  Each change list (padded to a multiple of 16) is
-  // staged in the slot area, which is free until step 2; with B < NT the NT / B thread groups
-  // take contiguous parts of a list and their partial sums are added in group order.
+  // earlier ones' changes are in the residual the launch started from).  The persistent solver
+  // keeps the lists in LDS (written by its own write-back); the per-block solve stages the one list
+  // of its lag-1 pipeline from global memory into the slot area, which is free until step 2.  Every
+  // list's cross-Gram loads are issued together (one round trip per 16 entries, not per list).
+  // With B < NT the NT / B thread groups take contiguous parts of each list and their partial sums
+  // are added in group order.
   constexpr int PG = B < NT ? NT / B : 1;
   double *scr = resident ? slots + (int64_t)B * B : slots;
-  double *Lcd = scr;
-  int *Lcg = reinterpret_cast<int *>(scr + (B + 16));
-  double *Lpart = scr + (B + 16) + (B + 16) / 2 + 1;
+  double *Lpart = scr + (B + 16) + (B + 16) / 2 + 1;  // [PG][B] partial sums (PG > 1)
   const int nlist = d.lag;
-  for (int l = 0; l < nlist; ++l) {
+  const double *Cl[LAG_MAX] = {nullptr, nullptr, nullptr};
+  const double *Ldl[LAG_MAX] = {nullptr, nullptr, nullptr};
+  const int *Lgl[LAG_MAX] = {nullptr, nullptr, nullptr};
+  int npl[LAG_MAX] = {0, 0, 0};
+  bool staged = false;
+#pragma unroll
+  for (int l = 0; l < LAG_MAX; ++l) {
     const int sp = s - 1 - l;  // the earlier block
-    if (l > 0 && sp < d.seg0) break;
-    if (l > 0) __syncthreads();  // every thread is done with the previous list's staging / partials
-    const double *C = nullptr;
-    int np_prev = 0;
-    if (sp >= d.seg0) {
-      const int gp = d.gblk[sp];
-      if (l == 0)
-        C = (gb == (gp + 1) % d.nb) ? d.xgram + (int64_t)gp * B * B : d.xgramT + (int64_t)gb * B * B;
-      else if (l == 1)
-        C = (gb == (gp + 2) % d.nb) ? d.xgram2 + (int64_t)gp * B * B : d.xgram2T + (int64_t)gb * B * B;
-      else
-        C = (gb == (gp + 3) % d.nb) ? d.xgram3 + (int64_t)gp * B * B : d.xgram3T + (int64_t)gb * B * B;
-      if (persistent && resident && l == 0 && s > d.seg0 && misc[11] == s - 1) {
-        // this workgroup wrote block s-1's list into Lcg / Lcd itself (step 4 of that block,
-        // persistent solver): no global round trip
-        np_prev = misc[10];
-      } else {
-        const int slot = sp % NSLOT;
-        np_prev = ld_sc1_int(d.pend_n + slot);  // written with sc1 stores by that block's solve
-        const int *pv_gi = d.pend_gi + slot * d.pend_stride;
-        const double *pv_bo = d.pend_bo + slot * d.pend_stride, *pv_bn = d.pend_bn + slot * d.pend_stride;
-        for (int e = t; e < np_prev; e += NT) {
-          Lcg[e] = ld_sc1_int(pv_gi + e);
-          Lcd[e] = ld_sc1(pv_bn + e) - ld_sc1(pv_bo + e);
+    if (l >= nlist || sp < d.seg0) continue;
+    const int gp = d.gblk[sp];
+    if (l == 0)
+      Cl[l] = (gb == (gp + 1) % d.nb) ? d.xgram + (int64_t)gp * B * B : d.xgramT + (int64_t)gb * B * B;
+    else if (l == 1)
+      Cl[l] = (gb == (gp + 2) % d.nb) ? d.xgram2 + (int64_t)gp * B * B : d.xgram2T + (int64_t)gb * B * B;
+    else
+      Cl[l] = (gb == (gp + 3) % d.nb) ? d.xgram3 + (int64_t)gp * B * B : d.xgram3T + (int64_t)gb * B * B;
+    const int j = nlb > 0 ? sp % nlb : 0;
+    if (nlb > 0 && misc[17 + 2 * j] == sp) {
+      // this workgroup wrote block sp's list into LDS buffer j itself (its step 4)
+      npl[l] = misc[16 + 2 * j];
+      Ldl[l] = Llist + (int64_t)j * (B + 16);
+      Lgl[l] = Lligi + (int64_t)j * (B + 16);
+    } else if (!staged) {
+      // (per-block solve: lag 1, one list) from global memory, written with sc1 stores
+      double *Lcd = scr;
+      int *Lcg = reinterpret_cast<int *>(scr + (B + 16));
+      const int slot = sp % NSLOT;
+      const int np = ld_sc1_int(d.pend_n + slot);
+      const int *pv_gi = d.pend_gi + slot * d.pend_stride;
+      const double *pv_bo = d.pend_bo + slot * d.pend_stride, *pv_bn = d.pend_bn + slot * d.pend_stride;
+      for (int e = t; e < np; e += NT) {
+        Lcg[e] = ld_sc1_int(pv_gi + e);
+        Lcd[e] = ld_sc1(pv_bn + e) - ld_sc1(pv_bo + e);
+      }
+      npl[l] = np;
+      Ldl[l] = Lcd;
+      Lgl[l] = Lcg;
+      staged = true;
+    }
+  }
+  if (staged) __syncthreads();
+#pragma unroll
+  for (int c = 0; c < NPT; ++c) {
+    const int pos = (t % (B < NT ? B : NT)) + NT * c;
+    const int grp = B < NT ? t / B : 0;
+    double corr[LAG_MAX] = {0.0, 0.0, 0.0};
+    if (pos < bs) {
+      const int gi = NPT == 1 ? gi_t : Lgi[pos];
+      int c0[LAG_MAX], c1[LAG_MAX];
+#pragma unroll
+      for (int l = 0; l < LAG_MAX; ++l) {
+        const int nch = npl[l] / 16;
+        c0[l] = grp * nch / PG;
+        c1[l] = (grp + 1) * nch / PG;
+      }
+      // per round: the next chunk (16 entries) of every list in flight, then added in list order
+      for (int k = 0;; ++k) {
+        bool more = false;
+        double cv[LAG_MAX][16];
+#pragma unroll
+        for (int l = 0; l < LAG_MAX; ++l) {
+          const int ch = c0[l] + k;
+          if (ch < c1[l]) {
+            more = true;
+#pragma unroll
+            for (int u = 0; u < 16; ++u) cv[l][u] = Cl[l][(int64_t)Lgl[l][16 * ch + u] * B + gi];
+          }
+        }
+        if (!more) break;
+#pragma unroll
+        for (int l = 0; l < LAG_MAX; ++l) {
+          const int ch = c0[l] + k;
+          if (ch < c1[l]) {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) corr[l] += cv[l][u] * Ldl[l][16 * ch + u];
+          }
         }
       }
     }
+    // the lists' sums added in list order (per thread group, then the groups in group order)
+    const double tot = (corr[0] + corr[1]) + corr[2];
+    if (PG == 1) {
+      if (pos < bs) Lr0[pos] = tot;
+    } else {
+      Lpart[grp * B + pos] = tot;
+    }
+  }
+  if (PG > 1) {
     __syncthreads();
+    if (t < bs) {
+      double tot = Lpart[t];
 #pragma unroll
-    for (int c = 0; c < NPT; ++c) {
-      const int pos = (t % (B < NT ? B : NT)) + NT * c;
-      const int grp = B < NT ? t / B : 0;
-      const int nch = np_prev / 16;
-      const int c0 = grp * nch / PG, c1 = (grp + 1) * nch / PG;
-      double corr = 0.0;
-      if (pos < bs) {
-        const int gi = NPT == 1 ? gi_t : Lgi[pos];
-        // two chunks (32 loads) in flight, added in list order
-        for (int ch = c0; ch < c1; ch += 2) {
-          const bool two = ch + 1 < c1;
-          double cv[32];
-#pragma unroll
-          for (int u = 0; u < 16; ++u) cv[u] = C[(int64_t)Lcg[16 * ch + u] * B + gi];
-          if (two) {
-#pragma unroll
-            for (int u = 0; u < 16; ++u) cv[16 + u] = C[(int64_t)Lcg[16 * ch + 16 + u] * B + gi];
-          }
-#pragma unroll
-          for (int u = 0; u < 16; ++u) corr += cv[u] * Lcd[16 * ch + u];
-          if (two) {
-#pragma unroll
-            for (int u = 0; u < 16; ++u) corr += cv[16 + u] * Lcd[16 * ch + 16 + u];
-          }
-        }
-      }
-      if (PG == 1) {
-        if (pos < bs) Lr0[pos] = l == 0 ? corr : Lr0[pos] + corr;
-      } else {
-        Lpart[grp * B + pos] = corr;
-      }
-    }
-    if (PG > 1) {
-      __syncthreads();
-      if (t < bs) {
-        double corr = Lpart[t];
-#pragma unroll
-        for (int g = 1; g < PG; ++g) corr += Lpart[g * B + t];
-        Lr0[t] = l == 0 ? corr : Lr0[t] + corr;
-      }
+      for (int g = 1; g < PG; ++g) tot += Lpart[g * B + t];
+      Lr0[t] = tot;
     }
   }
   const uint64_t tA2 = prof ? wall_clock64() : 0;  // cross-Gram correction done
@@ -2107,9 +2144,9 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       st_sc1_int(ppos + idx, pos);
       st_sc1(pbo + idx, bov);
       st_sc1(pbn + idx, bnv);
-      if (resident) {  // the next block's cross-Gram correction reads it from LDS (phase A)
-        Lcg[idx] = Lgi[pos];
-        Lcd[idx] = bnv - bov;
+      if (nlb > 0) {  // the next blocks' cross-Gram corrections read it from LDS (phase A)
+        Llist[(int64_t)(s % nlb) * (B + 16) + idx] = bnv - bov;
+        Lligi[(int64_t)(s % nlb) * (B + 16) + idx] = Lgi[pos];
       }
     }
     for (int w = 0; w < NW; ++w) base += misc[w];
@@ -2117,9 +2154,12 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   }
   const int npend = base;
   const int npad = (npend + 15) & ~15;  // lists are read in batches of 8 / 16
-  if (resident) {
-    if (npend + t < npad) { Lcg[npend + t] = 0; Lcd[npend + t] = 0.0; }
-    if (t == 0) { misc[10] = npad; misc[11] = s; }
+  if (nlb > 0) {
+    if (npend + t < npad) {
+      Llist[(int64_t)(s % nlb) * (B + 16) + npend + t] = 0.0;
+      Lligi[(int64_t)(s % nlb) * (B + 16) + npend + t] = 0;
+    }
+    if (t == 0) { misc[16 + 2 * (s % nlb)] = npad; misc[17 + 2 * (s % nlb)] = s; }
   }
   if (npend + t < npad) {  // neutral padding: eps + x*0 - x*0 == eps exactly, delta = 0
     st_sc1_int(pidx + npend + t, 0);
@@ -3212,7 +3252,7 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   if (split && hipFuncGetAttributes(&attr_st, fst) != hipSuccess) return false;
   const size_t budget = SOLVE_LDS_MAX - attr.sharedSizeBytes;
   const int K = d.model == MODEL_HORSESHOE ? 1 : d.K;
-  const size_t fixed = solve_fixed_bytes(d.B, K);
+  const size_t fixed = solve_fixed_bytes(d.B, K, d.lag);  // (the persistent solver keeps d.lag lists in LDS)
   if (fixed + 8 * (size_t)d.B > budget) return false;
   const int snt = split ? SOLVE_NT : SWEEP_NT;  // the solver workgroup's threads
   const int nslot = (int)std::min<size_t>((size_t)solve_max_slots(d.B, snt), (budget - fixed) / (8 * (size_t)d.B));
