@@ -51,9 +51,11 @@ struct Scal {
   double S1;   // sum(eps + mu)   (BayesRv2.cpp:177-178 operand), from the latest row pass
   double S2;   // ||eps||^2        (BayesRv2.cpp:251 operand)
   double fx;   // row shards: this shard's part of a fixed-effect dot (BayesRv2Groups.cpp:220), summed across shards
-  int pad0, pad1;
+  int lag_next;  // pipeline lag of the next fused sweep: 2 = Dev::lag, else 1 (set by k_hyper, see Dev::lag_thresh)
+  int pad1;
   unsigned long long n_slow;     // diagnostics: serial steps that needed the exact re-evaluation
-  unsigned long long n_changed;  // diagnostics: markers whose beta changed
+  unsigned long long n_changed;  // markers whose beta changed (session total)
+  unsigned long long nch_mark;   // n_changed at the end of the previous sweep
   int prof_on;                   // diagnostics: k_solve phase timers on
   int pad2;
   unsigned long long prof[16];   // k_solve phase totals (wall_clock64 ticks, 100 MHz), counters
@@ -117,7 +119,9 @@ struct Dev {
   double *gram, *xgram, *xgramT;
   double *xgram2, *xgram2T;  // lag >= 2: X_b^T X_{b+2 mod nb} and its transpose (else nullptr)
   double *xgram3, *xgram3T;  // lag 3: X_b^T X_{b+3 mod nb} and its transpose (else nullptr)
-  int lag;                   // pipeline lag L (1 or 2, see NPAR)
+  int lag;                   // pipeline lag L (1 or 2, see NPAR): the fused sweep's largest (LDS layout)
+  double lag_thresh;         // changes in a sweep above which the next fused sweep runs lag 1: its solver
+                             // is then the bottleneck (burn-in), and lag 1 halves its cross-Gram work
   int *member, *gidx, *bsz, *gblk, *blkorder;
   double *slab1, *slab2;   // [2][RG*B], [2][NGpad*B]
   int *cnt1;                // [2][NG*NC] level-2 arrival counters (k_stream), cumulative

@@ -1192,6 +1192,10 @@ __device__ __forceinline__ int reduce16_col(int lane) {
 //   slots    nslot Gram rows (B doubles each), staged for the positions predicted to change
 enum PrFlag : int { PF_EX = 1 << 8, PF_LIKELY = 1 << 9 };
 
+// pipeline lag of this fused sweep: Dev::lag, or 1 while the previous sweep changed many markers
+// (k_hyper sets Scal::lag_next; 0 before the first sweep = 1).  Both kernels of a sweep read it once.
+__device__ __forceinline__ int sweep_lag(const Dev &d) { return d.sc->lag_next >= 2 ? d.lag : 1; }
+
 // nlb: change-list buffers kept in LDS from block to block (persistent solver: one per pipeline lag,
 // block s's list in buffer s % nlb, each B + 16 doubles of deltas and B + 16 Gram indices)
 __host__ __device__ inline size_t solve_fixed_bytes(int B, int K, int nlb = 0) {
@@ -1541,7 +1545,7 @@ template <bool HS, int B, int NT>
 // gi_pref: (persistent) the Gram index of position threadIdx.x % B of the next block, loaded one
 // block ahead so the next block's cross-Gram loads need no dependent round trip
 __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, int nslot, char *smem,
-                                            bool persistent, int &gi_pref) {
+                                            bool persistent, int &gi_pref, int lag) {
 #pragma clang fp contract(off)
   constexpr int NPT = (B + NT - 1) / NT;  // positions per thread, parallel phases
   constexpr int NW = NT / 64;             // waves
@@ -1640,7 +1644,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   constexpr int PG = B < NT ? NT / B : 1;
   double *scr = resident ? slots + (int64_t)B * B : slots;
   double *Lpart = scr + (B + 16) + (B + 16) / 2 + 1;  // [PG][B] partial sums (PG > 1)
-  const int nlist = d.lag;
+  const int nlist = lag;  // (<= d.lag: the persistent solver's lag of this sweep; per-block: 1)
   const double *Cl[LAG_MAX] = {nullptr, nullptr, nullptr};
   const double *Ldl[LAG_MAX] = {nullptr, nullptr, nullptr};
   const int *Lgl[LAG_MAX] = {nullptr, nullptr, nullptr};
@@ -2203,7 +2207,7 @@ template <bool HS, int B>
 __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it, int nslot) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int gi_pref = 0;
-  solve_block<HS, B, 256>(d, s, it, nslot, smem, false, gi_pref);
+  solve_block<HS, B, 256>(d, s, it, nslot, smem, false, gi_pref, d.lag);
 }
 
 
@@ -2489,7 +2493,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   const bool prof = d.sc->prof_on;
   // 2-bit storage: the value tables of blocks s - 2 .. s + 1 in LDS (buffer s & 3): block s + 1's
   // are staged at boundary s (inside the apply), block s - 2's serve the apply
-  const int LAG = d.lag;
+  const int LAG = sweep_lag(d);  // (buffer counts below are within the layout's d.lag)
   const int NLB = LAG + 3;  // value-table buffers: blocks s-1-LAG (apply) .. s+1 (staged)
   const int NCC = LAG + 2;  // code-cache buffers: blocks s-1-LAG (apply) .. s (being streamed)
   // (a column's table: its 4 f32 values as doubles, read per value by code, so a product is the
@@ -2787,8 +2791,9 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
 template <bool HS, int B, int NT = SWEEP_NT>
 __device__ BRR_SOLVER_INL void solver_role(const Dev &d, uint32_t it, int nslot, char *smem) {
   int gi_pref = 0;
+  const int lag = sweep_lag(d);
   for (int s = d.seg0; s < d.seg1; ++s) {
-    solve_block<HS, B, NT>(d, s, it, nslot, smem, true, gi_pref);
+    solve_block<HS, B, NT>(d, s, it, nslot, smem, true, gi_pref, lag);
     __syncthreads();
   }
 }
@@ -2979,6 +2984,11 @@ __global__ void k_hyper(Dev d, uint32_t it, const double *stats) {
   const double *v = stats + 2 + G;
   const double sigmaE_new = inv_scaled_chisq_rng(d.seed, h.v0E + N, (sc->S2 + h.v0E * h.s02E) / (h.v0E + N),
                                                  T_SIGMAE, 0, it);
+  if (t == 0) {  // the next fused sweep's pipeline lag from this sweep's changes (Dev::lag_thresh)
+    const unsigned long long nc = sc->n_changed;
+    sc->lag_next = (double)(nc - sc->nch_mark) > d.lag_thresh ? 1 : 2;
+    sc->nch_mark = nc;
+  }
   if (d.model == MODEL_HORSESHOE) {
     if (t == 0) {
       const double M = (double)d.M_total;
