@@ -18,12 +18,24 @@ import sys
 
 def main():
     tdir, skip, prefix = sys.argv[1], int(sys.argv[2]), sys.argv[3]
-    rows = []
+    rows, solve, stream, split = [], [], [], None
     for f in glob.glob(os.path.join(tdir, "**", "*kernel_trace.csv"), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                if "k_sweep<" in r.get("Kernel_Name", ""):
-                    rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+                kn = r.get("Kernel_Name", "")
+                if "k_sweep<" in kn:
+                    rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kn))
+                elif "k_sweep_solve<" in kn:
+                    solve.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kn))
+                elif "k_sweep_stream<" in kn:
+                    stream.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kn))
+    if not rows and solve and len(solve) == len(stream):
+        # the two-kernel sweep (k_sweep_solve beside k_sweep_stream, launched together): one sweep
+        # = the span from the first start to the last end of the pair
+        solve.sort()
+        stream.sort()
+        rows = [(min(a[0], b[0]), max(a[1], b[1]), "k_sweep_solve + " + b[2]) for a, b in zip(solve, stream)]
+        split = {"solve_us": [(e - s) / 1e3 for s, e, _ in solve], "stream_us": [(e - s) / 1e3 for s, e, _ in stream]}
     rows.sort()
     if not rows:
         sys.exit("no k_sweep dispatches in the trace")
@@ -36,6 +48,9 @@ def main():
     out = {"kernel": rows[0][2][:80], "dispatches": len(dur), "skipped_burn_in": skip, "calls": len(ss),
            "mean_us": sum(ss) / len(ss), "min_us": min(ss), "max_us": max(ss),
            "all_dispatch_mean_us": sum(dur) / len(dur)}
+    if split:
+        for k, v in split.items():
+            out["steady_" + k.replace("_us", "_mean_us")] = sum(v[skip:]) / len(v[skip:])
     with open(prefix + "_steady.json", "w") as fh:
         json.dump(out, fh, indent=1)
     print(prefix, json.dumps(out))
