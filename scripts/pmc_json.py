@@ -21,10 +21,10 @@ def per_dispatch(d, counter):
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 kn = r.get("Kernel_Name", "")
-                if r.get("Counter_Name") == counter and ("k_sweep<" in kn or "k_sweep_s" in kn):
+                if r.get("Counter_Name") == counter and ("k_sweep<" in kn or "k_sweep_solve<" in kn or "k_sweep_stream<" in kn):
                     rows.append((int(r.get("Dispatch_Id", 0) or 0), float(r["Counter_Value"]), kn))
     rows.sort()
-    if any("k_sweep_s" in k for _, _, k in rows):
+    if any("k_sweep_stream<" in k for _, _, k in rows):
         # the two-kernel sweep: k_sweep_solve and k_sweep_stream of one sweep are launched back to
         # back (consecutive dispatch ids); a sweep's traffic is the sum of the pair
         sv = [v for _, v, k in rows if "k_sweep_solve" in k]

@@ -41,11 +41,14 @@ if [ "${SOLVE:-0}" = 1 ]; then
 fi
 if [ "${REF:-0}" = 1 ]; then
   # where a REFERENCE-order sweep's time goes (Gram blocks recomputed every sweep)
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_ref -o run --output-format csv \
-    -- python3 bench.py --order reference --steps 2 --warmup 1 --no-roofline-events $ARGS > gpurun_out/${TAG}_ref.log 2>&1 \
-    || { echo "REF FAILED"; tail -30 gpurun_out/${TAG}_ref.log; exit 1; }
-  cut -c1-160 $(find gpurun_out/${TAG}_ref -name "*kernel_stats.csv" | head -1) | head -8
-  tail -1 gpurun_out/${TAG}_ref.log | cut -c1-300
+  for rb in ${REF_B:-512 128}; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_ref$rb -o run --output-format csv \
+      -- python3 bench.py --order reference --block-size $rb --steps 2 --warmup 1 --no-roofline-events $ARGS > gpurun_out/${TAG}_ref$rb.log 2>&1 \
+      || { echo "REF FAILED"; tail -30 gpurun_out/${TAG}_ref$rb.log; exit 1; }
+    echo "== reference order B = $rb"
+    cut -c1-160 $(find gpurun_out/${TAG}_ref$rb -name "*kernel_stats.csv" | head -1) | head -8
+    tail -1 gpurun_out/${TAG}_ref$rb.log | cut -c1-300
+  done
 fi
 if [ "${EXITCRASH:-0}" = 1 ]; then
   BRR_FUSED_SINGLE=1 BRR_SEGV_TRACE=1 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_exit -o run --output-format csv \
