@@ -14,7 +14,8 @@
 //            inputs; a sweep reads N P / 4 bytes instead of 4 N P.
 //   eps,eps2 f64 [ld] residual (Y - mu - X beta), double-buffered across k_stream launches.
 //   beta,xsq f64 [M]; comp int32 [M]; sel uint8 [M] (marker selected a component this sweep)
-//   gram     f64 [nb][B][B] block Gram matrices X_b^T X_b of the fixed column blocks.
+//   gram     f64 [nb][B][B] block Gram matrices X_b^T X_b of the fixed column blocks (for
+//            class-coded columns the exact dot products, correctly rounded: k_gram_int).
 //   xgram    f64 [nb][B][B] cross-Gram X_b^T X_{b+1 mod nb} of cycle neighbours; xgramT its
 //            transposes (rows indexed by block b+1).  Consecutive blocks of a sweep are cycle
 //            neighbours (visit order = rotation of the block cycle, either direction).
@@ -109,6 +110,14 @@ struct Dev {
                        // row i in bits 2(i&3)..2(i&3)+1 of byte i>>2 (PLINK .bed packing)
   const float *xlut;   // [M][4] value of each code of column j (padding rows decode to 0)
   int64_t ldc;         // bytes per code column = ld / 4
+  // value classes of every column (k_classes): the distinct values of its N rows, ascending, when a
+  // column has at most 4 of them (genotype columns, in either storage) -- the integer Gram kernel
+  // (k_gram_int) counts class pairs on the i8 matrix cores and forms each Gram entry exactly
+  int *cls_info;       // [M] ncls (bits 0-2; 0 = not class-coded) | code -> class map << 8 (2-bit storage)
+  float *cls_val;      // [M][4] class values, ascending (classes >= ncls: 0)
+  int *cls_cnt;        // [M][4] real rows in each class
+  int gram_np;         // k_gram_int's explicit class planes (1..3); 0 = the f64 matrix-core k_gram
+  uint8_t *gram_codes; // k_gram_int's input: [nb][B/16][ldc][16] class codes of the current layout (k_encode_layout)
   const double *Y, *fixed, *cva;
   const int *gAssign;
   double *eps, *eps2, *eps_start, *deps, *beta, *xsq, *lambda, *hsv, *sigmaGG, *pi, *alpha;

@@ -431,6 +431,372 @@ __global__ __launch_bounds__(256) void k_gram(Dev d, const int *member, const in
       }
 }
 
+// ------------------------------------------------------------------------------------
+// Value classes of a column ("integer Gram"): the distinct values of its N rows,
+// ascending, with their row counts, when there are at most 4 -- genotype columns in either storage
+// (2-bit: the table values of the codes that occur; f32: the values themselves, so both storages
+// give the same classes).  Rejected (cls_info = 0): more than 4 values, or nonzero values whose
+// binary exponents span more than 20 (k_gram_int sums exactly in 128 bits).  flags[0] |= 1 for a
+// rejected column, flags[1] = max ncls.
+__device__ __forceinline__ int f32_key(float v) {  // order-preserving int of a float (+0 for -0)
+  const int b = __float_as_int(v == 0.f ? 0.f : v);
+  return b >= 0 ? b : b ^ 0x7FFFFFFF;
+}
+__device__ __forceinline__ float key_f32(int k) { return __int_as_float(k >= 0 ? k : k ^ 0x7FFFFFFF); }
+
+__global__ __launch_bounds__(256) void k_classes(Dev d, int *flags) {
+  const int64_t j = blockIdx.x;
+  const int t = threadIdx.x;
+  __shared__ int s_key[5], s_cnt[4], s_n, s_over, s_min;
+  float lv[4] = {0.f, 0.f, 0.f, 0.f};  // this thread's distinct values and their rows
+  int lc[4] = {0, 0, 0, 0};
+  int ln = 0;
+  bool over = false;
+  if (d.Xc) {
+    // the codes' row counts; each code is one value of the column's table
+    for (int64_t g = t; 4 * g < d.N; g += 256) {
+      const uint32_t b = d.Xc[code_off(j, g, d.B, d.ldc)];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t cd = (b >> (2 * k)) & 3u;
+        const int in = 4 * g + k < d.N;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lc[q] += (cd == (uint32_t)q) ? in : 0;
+      }
+    }
+    const float4 l = x_lut(d, j);
+    lv[0] = l.x; lv[1] = l.y; lv[2] = l.z; lv[3] = l.w;
+    ln = 4;  // (codes that never occur have no rows and are skipped below)
+  } else {
+    const float *x = d.X + j * d.ld;
+    for (int64_t i = t; i < d.N; i += 256) {
+      const float v = x[i] == 0.f ? 0.f : x[i];
+      int k = -1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) k = (q < ln && lv[q] == v) ? q : k;
+      if (k >= 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) lc[q] += q == k;
+      } else if (ln < 4 && v == v) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (q == ln) { lv[q] = v; lc[q] = 1; }
+        ++ln;
+      } else {
+        over = true;  // a fifth value, or NaN
+      }
+    }
+  }
+  if (t == 0) { s_n = 0; s_over = 0; }
+  if (t < 4) s_cnt[t] = 0;
+  __syncthreads();
+  if (over) s_over = 1;
+  // the classes in ascending order: every round adds the smallest value not yet a class
+  for (int r = 0; r < 5; ++r) {
+    if (t == 0) s_min = 0x7FFFFFFF;
+    __syncthreads();
+    const int nk = s_n;
+    int mine = 0x7FFFFFFF;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q >= ln || lc[q] == 0) continue;
+      const int key = f32_key(lv[q]);
+      bool seen = false;
+      for (int c = 0; c < nk; ++c) seen |= s_key[c] == key;
+      if (!seen) mine = min(mine, key);
+    }
+    if (mine != 0x7FFFFFFF) atomicMin(&s_min, mine);
+    __syncthreads();
+    const int m = s_min;
+    __syncthreads();
+    if (m == 0x7FFFFFFF) break;
+    if (t == 0) {
+      if (nk < 4) s_key[nk] = m; else s_over = 1;
+      s_n = nk + 1;
+    }
+    __syncthreads();
+    if (s_n > 4) break;
+  }
+  const int nc = min(s_n, 4);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (q >= ln || lc[q] == 0) continue;
+    const int key = f32_key(lv[q]);
+    for (int c = 0; c < nc; ++c)
+      if (s_key[c] == key) atomicAdd(&s_cnt[c], lc[q]);
+  }
+  __syncthreads();
+  if (t == 0) {
+    bool bad = s_over != 0 || s_n > 4;
+    int emin = 1 << 20, emax = -(1 << 20);
+    for (int c = 0; c < nc; ++c) {
+      const float v = key_f32(s_key[c]);
+      if (v != 0.f) {
+        int e;
+        frexpf(v, &e);
+        emin = min(emin, e);
+        emax = max(emax, e);
+      }
+    }
+    if (emax - emin > 20) bad = true;
+    int cmap = 0;  // 2-bit storage: class of each code (codes without rows: 0)
+    if (d.Xc && !bad) {
+      const float4 l = x_lut(d, j);
+      const float tv[4] = {l.x, l.y, l.z, l.w};
+      for (int k = 0; k < 4; ++k)
+        for (int c = 0; c < nc; ++c)
+          if (s_key[c] == f32_key(tv[k])) cmap |= c << (2 * k);
+    }
+    d.cls_info[j] = bad ? 0 : (nc | cmap << 8);
+    for (int c = 0; c < 4; ++c) {
+      d.cls_val[4 * j + c] = (!bad && c < nc) ? key_f32(s_key[c]) : 0.f;
+      d.cls_cnt[4 * j + c] = (!bad && c < nc) ? s_cnt[c] : 0;
+    }
+    if (bad) atomicOr(flags, 1);
+    atomicMax(flags + 1, bad ? 0 : nc);
+  }
+}
+
+// Class codes of the current Gram layout (k_gram_int's input): byte of (block position b, in-block
+// index i, row quad g) at code_off(b B + i, g) of Xk = the classes (2 bits per row) of the 4 rows of
+// column member[b B + i] -- the column's value classes looked up from its 2-bit codes or found by
+// comparing its f32 values with the class values.  A block's columns are then 16-B groups in row
+// order whatever columns the visit order put in it (REFERENCE order re-encodes every sweep).
+// Thread: (position group of 16, row quad); 16 columns' classes written as one 16-B store.
+__global__ __launch_bounds__(256) void k_encode_layout(Dev d, uint8_t *Xk) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int ng = d.B / 16;
+  for (int64_t bq = blockIdx.y; bq < (int64_t)d.nb * ng; bq += gridDim.y) {
+    if (g >= d.ldc) return;
+    const int b = (int)(bq / ng), q = (int)(bq % ng);
+    const int bs = d.bsz[b];
+    uint32_t out[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int pos = 16 * q + i;
+      uint32_t byte = 0;
+      if (pos < bs && 4 * g < d.N) {
+        const int64_t col = d.member[(int64_t)b * d.B + pos];
+        const int info = d.cls_info[col];
+        if (d.Xc) {
+          const uint32_t c = d.Xc[code_off(col, g, d.B, d.ldc)];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) byte |= (((uint32_t)info >> (8 + 2 * ((c >> (2 * k)) & 3u))) & 3u) << (2 * k);
+        } else {
+          const float4 x = *reinterpret_cast<const float4 *>(d.X + col * d.ld + 4 * g);
+          const int nc = info & 7;
+          const float *v = d.cls_val + 4 * col;
+          const float v1 = v[1], v2 = v[2], v3 = v[3];
+          auto cl = [&](float xv) -> uint32_t {
+            return (nc > 1 && xv == v1) ? 1u : (nc > 2 && xv == v2) ? 2u : (nc > 3 && xv == v3) ? 3u : 0u;
+          };
+          byte = cl(x.x) | cl(x.y) << 2 | cl(x.z) << 4 | cl(x.w) << 6;
+        }
+      }
+      out[i >> 2] |= byte << (8 * (i & 3));
+    }
+    *reinterpret_cast<uint4 *>(Xk + (bq * d.ldc + g) * 16) = make_uint4(out[0], out[1], out[2], out[3]);
+  }
+}
+
+// Exact integer Gram of class-coded columns on the i8 matrix cores.  For columns i, j with class
+// values u_a, w_b and n_ab = #rows where column i is in class a and column j in class b,
+//     G_ij = sum_ab n_ab u_a w_b
+// exactly: the NP x NP explicit counts are I_a^T I_b of 0/1 class indicator bytes
+// (v_mfma_i32_16x16x64_i8 over the rows, int32 accumulation is exact), the counts of the last
+// class follow from the per-column class totals, and the sum of the (NP+1)^2 integer multiples of
+// u_a w_b (each a 24-bit x 24-bit mantissa product times a power of two) is formed in a 128-bit
+// integer and rounded once -- the correctly rounded dot product of the f32 columns, in either
+// storage, in any order (symmetric on the diagonal blocks).  GI_T x GI_T output columns per
+// workgroup of 4 waves, each wave a quadrant of the (NP GI_T)^2 count matrix.  Input: the layout's
+// class codes (k_encode_layout), GI_KC-row chunks read as 16-B groups (16 columns x 4 rows) GI_D
+// chunks ahead in registers (a ring unrolled by its depth: each chunk waits for its own loads only),
+// expanded to indicator planes in LDS as [side][plane][column][row] bytes (pitch GI_KC + 16: the 16-B
+// operand reads of 16 consecutive columns hit 16 distinct 4-bank groups).
+constexpr int GI_T = 64;
+constexpr int GI_KC = 256;
+constexpr int GI_D = 4;
+constexpr int GI_PITCH = GI_KC + 16;
+__host__ __device__ constexpr size_t gram_int_lds(int NP) {
+  return (size_t)2 * NP * GI_T * GI_PITCH > (size_t)NP * GI_T * NP * GI_T * 4 ? (size_t)2 * NP * GI_T * GI_PITCH
+                                                                             : (size_t)NP * GI_T * NP * GI_T * 4;
+}
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+template <int NP>
+__global__ __launch_bounds__(256) void k_gram_int(Dev d, const uint8_t *Xk, const int *member, const int *bsz, int B,
+                                                  int nb, int shift, double *G, double *GT) {
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  uint8_t *stg = reinterpret_cast<uint8_t *>(gsm);  // the k loop's indicator planes
+  int *cntm = reinterpret_cast<int *>(gsm);         // then the count matrix [NP GI_T][NP GI_T]
+  __shared__ int s_emin[2][GI_T];
+  __shared__ uint32_t s_cv[2][GI_T / 16];  // column-group validity: bit i = column 16 q + i exists
+  __shared__ int s_h[2][GI_T][4], s_M[2][GI_T][4], s_E[2][GI_T][4];
+  const int gb = blockIdx.x, gb2 = (gb + shift) % nb;
+  const int ntile = B / GI_T;
+  const int ti = blockIdx.y / ntile, tj = blockIdx.y % ntile;
+  const int bs = bsz[gb], bs2 = bsz[gb2];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, wi = wv >> 1, wj = wv & 1;
+  const int64_t N = d.N, nq = d.ldc;
+  if (t < 2 * GI_T / 16) s_cv[t / (GI_T / 16)][t % (GI_T / 16)] = 0u;
+  __syncthreads();
+  if (t < 2 * GI_T) {
+    // this tile's columns: class tables, each class value as M 2^(E + emin) with M a 24-bit integer
+    const int side = t / GI_T, c = t % GI_T;
+    const int idx = (side ? tj : ti) * GI_T + c;
+    const int64_t col = idx < (side ? bs2 : bs) ? member[(int64_t)(side ? gb2 : gb) * B + idx] : -1;
+    const int nc = col >= 0 ? d.cls_info[col] & 7 : 0;
+    if (col >= 0) atomicOr(&s_cv[side][c / 16], 1u << (c % 16));
+    int emin = 1 << 20, E[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool in = col >= 0 && k < nc;
+      const float v = in ? d.cls_val[4 * col + k] : 0.f;
+      s_h[side][c][k] = in ? d.cls_cnt[4 * col + k] : 0;
+      int e = 0;
+      const float f = frexpf(v, &e);  // v = f 2^e, f in [0.5, 1)
+      s_M[side][c][k] = v != 0.f ? (int)(f * 16777216.0f) : 0;
+      E[k] = e - 24;
+      if (v != 0.f) emin = min(emin, E[k]);
+    }
+    if (emin == (1 << 20)) emin = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s_E[side][c][k] = s_M[side][c][k] != 0 ? E[k] - emin : 0;
+    s_emin[side][c] = emin;
+  }
+  __syncthreads();
+  constexpr int W = NP * GI_T;  // count matrix rows (plane a, column i) = a GI_T + i; columns likewise
+  constexpr int NQ = W / 2 / 16;  // 16 x 16 count tiles per wave and dimension
+  i32x4 acc[NQ][NQ];
+#pragma unroll
+  for (int p = 0; p < NQ; ++p)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[p][q] = i32x4{0, 0, 0, 0};
+  // loader elements (side, column group q, row quad g), g fastest: one 16-B group of codes each
+  constexpr int QPC = GI_KC / 4;                   // row quads per chunk
+  constexpr int EPT = 2 * (GI_T / 16) * QPC / 256;  // elements per thread and chunk
+  static_assert(EPT * 256 == 2 * (GI_T / 16) * QPC, "whole loader rounds");
+  const int64_t nch = (N + GI_KC - 1) / GI_KC;
+  const uint4 *src[EPT];
+  int e_side[EPT], e_q[EPT], e_g[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    const int e = t + 256 * k;
+    e_g[k] = e % QPC;
+    e_q[k] = (e / QPC) % (GI_T / 16);
+    e_side[k] = e / (QPC * (GI_T / 16));
+    const int64_t grp = (int64_t)(e_side[k] ? gb2 : gb) * (B / 16) + (e_side[k] ? tj : ti) * (GI_T / 16) + e_q[k];
+    src[k] = reinterpret_cast<const uint4 *>(Xk) + grp * nq + e_g[k];
+  }
+  auto load = [&](int64_t ch, uint4 (&r)[EPT]) __attribute__((always_inline)) {
+    const int64_t c = ch < nch ? ch : nch - 1;  // (clamped: an unconditional load per slot)
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) r[k] = src[k][min(c * QPC + e_g[k], nq - 1) - e_g[k]];
+  };
+  uint4 ring[GI_D][EPT];
+#pragma unroll
+  for (int u = 0; u < GI_D; ++u) load(u, ring[u]);
+  for (int64_t c0 = 0; c0 < nch; c0 += GI_D) {
+#pragma unroll
+    for (int u = 0; u < GI_D; ++u) {
+      const int64_t ch = c0 + u;
+      if (ch >= nch) break;
+      // expand: per column of the group, 4 rows' classes -> one 0/1 byte per row and plane
+#pragma unroll
+      for (int k = 0; k < EPT; ++k) {
+        const int64_t row4 = ch * GI_KC + 4 * e_g[k];
+        const uint32_t vr = row4 >= N ? 0u : row4 + 4 <= N ? 0x01010101u : (0x01010101u >> (8 * (int)(4 - (N - row4))));
+        const uint32_t cv = s_cv[e_side[k]][e_q[k]];
+        const uint32_t wd[4] = {ring[u][k].x, ring[u][k].y, ring[u][k].z, ring[u][k].w};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t b = (wd[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+          const uint32_t cls = (b & 3u) | (b & 0xCu) << 6 | (b & 0x30u) << 12 | (b & 0xC0u) << 18;
+          const uint32_t valid = ((cv >> i) & 1u) ? vr : 0u;
+          uint8_t *dst = stg + (e_side[k] * NP * GI_T + 16 * e_q[k] + i) * GI_PITCH + 4 * e_g[k];
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {
+            const uint32_t x = cls ^ (0x01010101u * (uint32_t)p);
+            *reinterpret_cast<uint32_t *>(dst + p * GI_T * GI_PITCH) = ~(x | (x >> 1)) & valid;
+          }
+        }
+      }
+      load(ch + GI_D, ring[u]);  // this slot's next chunk, in flight during the products
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < GI_KC / 64; ++kk) {
+        i32x4 a[NQ], bb[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const int R = wi * (W / 2) + 16 * q, C = wj * (W / 2) + 16 * q;
+          a[q] = *reinterpret_cast<const i32x4 *>(stg + ((0 * NP + R / GI_T) * GI_T + R % GI_T + (lane & 15)) * GI_PITCH +
+                                                   kk * 64 + 16 * (lane >> 4));
+          bb[q] = *reinterpret_cast<const i32x4 *>(stg + ((1 * NP + C / GI_T) * GI_T + C % GI_T + (lane & 15)) * GI_PITCH +
+                                                    kk * 64 + 16 * (lane >> 4));
+        }
+#pragma unroll
+        for (int p = 0; p < NQ; ++p)
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) acc[p][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[p], bb[q], acc[p][q], 0, 0, 0);
+      }
+      __syncthreads();
+    }
+  }
+  // C/D map of the 16 x 16 MFMA: element r of lane l is (row 4 (l >> 4) + r, column l & 15)
+#pragma unroll
+  for (int p = 0; p < NQ; ++p)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        cntm[(wi * (W / 2) + 16 * p + 4 * (lane >> 4) + r) * W + wj * (W / 2) + 16 * q + (lane & 15)] = acc[p][q][r];
+  __syncthreads();
+  double *g = G + (int64_t)gb * B * B;
+  double *gt = GT ? GT + (int64_t)gb * B * B : nullptr;
+  for (int e = t; e < GI_T * GI_T; e += 256) {
+    const int i = e / GI_T, j = e % GI_T;
+    const int ii = ti * GI_T + i, jj = tj * GI_T + j;
+    double v = 0.0;
+    if (ii < bs && jj < bs2) {
+      int64_t n[NP + 1][NP + 1];
+      int64_t hi = 0;
+#pragma unroll
+      for (int a = 0; a < NP; ++a) {
+        int64_t sa = 0;
+#pragma unroll
+        for (int b = 0; b < NP; ++b) {
+          n[a][b] = cntm[(a * GI_T + i) * W + b * GI_T + j];
+          sa += n[a][b];
+        }
+        n[a][NP] = s_h[0][i][a] - sa;  // column j in the last class
+        hi += s_h[0][i][a];
+      }
+      int64_t sl = 0;
+#pragma unroll
+      for (int b = 0; b < NP; ++b) {
+        int64_t sb = 0;
+#pragma unroll
+        for (int a = 0; a < NP; ++a) sb += n[a][b];
+        n[NP][b] = s_h[1][j][b] - sb;  // column i in the last class
+        sl += n[NP][b];
+      }
+      n[NP][NP] = (N - hi) - sl;
+      __int128 s = 0;
+#pragma unroll
+      for (int a = 0; a <= NP; ++a)
+#pragma unroll
+        for (int b = 0; b <= NP; ++b) {
+          const int64_t m = (int64_t)s_M[0][i][a] * s_M[1][j][b];
+          if (n[a][b] != 0 && m != 0)
+            s += (__int128)n[a][b] * m * ((__int128)1 << (s_E[0][i][a] + s_E[1][j][b]));
+        }
+      v = ldexp((double)s, s_emin[0][i] + s_emin[1][j]);
+    }
+    g[(int64_t)ii * B + jj] = v;
+    if (gt) gt[(int64_t)jj * B + ii] = v;
+  }
+}
+
 __global__ void k_xsq_from_gram(const double *G, const int *member, const int *bsz, int B, int nb,
                                 double *xsq) {
   const int s = blockIdx.x;
@@ -3118,7 +3484,39 @@ hipError_t launch_cast_x(const void *src, bool is_f64, int64_t lds, float *dst, 
   return hipGetLastError();
 }
 
+hipError_t launch_classes(const Dev &d, int *flags, hipStream_t st) {
+  if (d.M <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_classes, dim3((unsigned)d.M), dim3(256), 0, st, d, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_encode_layout(const Dev &d, hipStream_t st) {
+  if (!d.gram_codes) return hipErrorInvalidValue;
+  const unsigned gy = (unsigned)std::min<int64_t>((int64_t)d.nb * (d.B / 16), 65535);
+  hipLaunchKernelGGL(k_encode_layout, dim3(cdiv64(d.ldc, 256), gy), dim3(256), 0, st, d, d.gram_codes);
+  return hipGetLastError();
+}
+
+template <int NP>
+static hipError_t launch_gram_int_t(const Dev &d, int shift, double *G, double *GT, hipStream_t st) {
+  constexpr size_t lds = gram_int_lds(NP);
+  static const hipError_t attr =
+      hipFuncSetAttribute((const void *)k_gram_int<NP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return attr;
+  const int nt = d.B / GI_T;
+  hipLaunchKernelGGL((k_gram_int<NP>), dim3((unsigned)d.nb, (unsigned)(nt * nt)), dim3(256), lds, st, d, d.gram_codes,
+                     d.member, d.bsz, d.B, d.nb, shift, G, GT);
+  return hipGetLastError();
+}
+
 hipError_t launch_gram(const Dev &d, int shift, double *G, double *GT, hipStream_t st) {
+  if (d.gram_np > 0 && d.gram_codes && d.B % GI_T == 0) {
+    switch (d.gram_np) {
+      case 1: return launch_gram_int_t<1>(d, shift, G, GT, st);
+      case 2: return launch_gram_int_t<2>(d, shift, G, GT, st);
+      default: return launch_gram_int_t<3>(d, shift, G, GT, st);
+    }
+  }
   const int nt = (d.B + GRAM_TILE - 1) / GRAM_TILE;
   static const hipError_t attr = hipFuncSetAttribute((const void *)k_gram, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                      (int)GRAM_LDS);

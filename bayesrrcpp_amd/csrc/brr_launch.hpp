@@ -18,6 +18,9 @@ hipError_t launch_cast_x(const void *src, bool is_f64, int64_t lds, float *dst, 
                          int64_t N, int64_t M, hipStream_t st);
 hipError_t launch_codes_tile(const uint8_t *src, uint8_t *Xc, int64_t c0, int64_t nc, int64_t ldc, int B,
                              hipStream_t st);
+hipError_t launch_classes(const Dev &d, int *flags, hipStream_t st);
+hipError_t launch_encode_layout(const Dev &d, hipStream_t st);  // class codes of the layout (Dev::gram_codes)
+// Gram blocks: k_gram_int (exact, i8 matrix cores) when Dev::gram_np > 0, else k_gram (FP64 MFMA)
 hipError_t launch_gram(const Dev &d, int shift, double *G, double *GT, hipStream_t st);
 hipError_t launch_xsq(const Dev &d, hipStream_t st);
 hipError_t launch_rows(const Dev &d, int flags, const double *deps_in, hipStream_t st,

@@ -179,6 +179,9 @@ struct brr_session {
   bool init_pending = false;  // column-shard restart between init_local and init_finish
   bool initialized = false, pi_given = false, need_reduce = false, have_y = false, have_x = false;
   bool x2bit = false;  // genotype storage: 2-bit codes (opt.x_storage == BRR_X_2BIT)
+  int *cls_flags = nullptr;  // k_classes: [0] a column is not class-coded, [1] max classes per column
+  uint8_t *gram_codes = nullptr;  // k_gram_int's input: class codes of the current Gram layout
+  int gram_np_init = 0;           // the Gram kernel of the latest init (Dev::gram_np then)
   double mu0 = 0, sigmaE0 = 0;
   double *ex_eps = nullptr, *ex_stats = nullptr;  // exchange buffers (caller- or session-owned)
   bool ex_owned = false;
@@ -212,6 +215,7 @@ struct brr_session {
     if (ev_x) (void)hipEventDestroy(ev_x);
     if (ev_go) (void)hipEventDestroy(ev_go);
     if (ev_done) (void)hipEventDestroy(ev_done);
+    if (gram_codes) (void)hipFree(gram_codes);
     if (st_side) (void)hipStreamSynchronize(st_side);
     if (st_side) (void)hipStreamDestroy(st_side);
     if (st) (void)hipStreamDestroy(st);
@@ -227,6 +231,8 @@ struct brr_session {
 };
 
 namespace {
+
+int encode_layout(brr_session *s);
 
 int rows_flagged(brr_session *s, int flags, const double *deps_in = nullptr) {
   HIPCHK(launch_rows(s->d, flags, deps_in, s->st));
@@ -356,6 +362,7 @@ int do_sweep_local(brr_session *s) {
       }
       s->grand.shuffle(s->ref_order);
       if (int rc = upload_order(s, shard_visit(s))) return rc;
+      if (int rc = encode_layout(s)) return rc;
       HIPCHK(launch_gram(d, 0, d.gram, nullptr, s->st));
       HIPCHK(launch_gram(d, 1, d.xgram, d.xgramT, s->st));
     } else {
@@ -563,11 +570,56 @@ int coll_each(Coll &c, F f) {
 
 double *sc_sums(brr_session *s) { return &s->d.sc->S1; }  // S1, S2: adjacent in Scal
 
+// Value classes of every column (k_classes) and the Gram kernel they allow: the exact integer
+// k_gram_int when every column has at most 4 distinct values (genotypes, either storage) and B is
+// a multiple of 64; else the FP64 k_gram.  BRR_GRAM_F64=1 forces the latter (diagnostics).
+int prepare_classes(brr_session *s) {
+  Dev &d = s->d;
+  d.gram_np = 0;
+  const char *f = getenv("BRR_GRAM_F64");
+  if ((f && f[0] == '1') || s->B % 64 != 0 || s->M == 0) return 0;
+  int fl[2] = {0, 0};
+  HIPCHK(hipMemsetAsync(s->cls_flags, 0, sizeof(int) * 2, s->st));
+  HIPCHK(launch_classes(d, s->cls_flags, s->st));
+  HIPCHK(hipStreamSynchronize(s->st));
+  HIPCHK(hipMemcpy(fl, s->cls_flags, sizeof fl, hipMemcpyDeviceToHost));
+  if (fl[0] == 0 && fl[1] >= 1) d.gram_np = std::max(1, fl[1] - 1);
+  if (d.gram_np > 0 && !s->gram_codes) {
+    // the layout's class codes: N P / 4 bytes (without them, the FP64 kernel)
+    if (hipMalloc(&s->gram_codes, (size_t)s->nb * s->B * d.ldc) != hipSuccess) {
+      (void)hipGetLastError();
+      s->gram_codes = nullptr;
+      d.gram_np = 0;
+    }
+  }
+  d.gram_codes = d.gram_np > 0 ? s->gram_codes : nullptr;
+  s->gram_np_init = d.gram_np;
+  return 0;
+}
+
+// Gram blocks of the current layout need its class codes first (k_gram_int)
+int encode_layout(brr_session *s) {
+  if (s->d.gram_np > 0) HIPCHK(launch_encode_layout(s->d, s->st));
+  return 0;
+}
+
+// BLOCKED / IDENTITY order: no Gram blocks after init, the class codes' memory is returned
+int release_gram_codes(brr_session *s) {
+  if (s->order_mode == BRR_ORDER_REFERENCE || !s->gram_codes) return 0;
+  HIPCHK(hipStreamSynchronize(s->st));
+  HIPCHK(hipFree(s->gram_codes));
+  s->gram_codes = nullptr;
+  s->d.gram_codes = nullptr;
+  s->d.gram_np = 0;
+  return 0;
+}
+
 // the Gram and cross-Gram blocks of the current layout (init; REFERENCE order: every sweep),
 // summed over the row shards
 int coll_grams(Coll &c) {
   if (int rc = coll_each(c, [](brr_session *s) -> int {
         Dev &d = s->d;
+        if (int rc = encode_layout(s)) return rc;
         HIPCHK(launch_gram(d, 0, d.gram, nullptr, s->st));
         HIPCHK(launch_gram(d, 1, d.xgram, d.xgramT, s->st));  // cycle neighbours (b, b+1 mod nb)
         if (d.lag >= 2) HIPCHK(launch_gram(d, 2, d.xgram2, d.xgram2T, s->st));  // (b, b+2 mod nb)
@@ -584,6 +636,7 @@ int coll_grams(Coll &c) {
 
 // last init step: hyper-parameter init draws from the (summed) statistics
 int init_finish(brr_session *s, const double *stats) {
+  if (int rc = release_gram_codes(s)) return rc;
   HIPCHK(launch_hyper_init(s->d, stats, s->pi_given, s->st));
   HIPCHK(hipStreamSynchronize(s->st));
   s->iteration = 0;
@@ -605,6 +658,7 @@ int coll_init(Coll &c, int32_t seed) {
         return 0;
       }))
     return rc;
+  if (int rc = coll_each(c, prepare_classes)) return rc;
   if (int rc = coll_grams(c)) return rc;
   if (int rc = coll_each(c, [](brr_session *s) -> int {
         Dev &d = s->d;
@@ -920,6 +974,10 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   rc |= s->alloc(&d.comp, M);
   rc |= s->alloc(&d.forder, std::max<int64_t>(F, 1));
   rc |= s->alloc(&d.sel, M);
+  rc |= s->alloc(&d.cls_info, M);
+  rc |= s->alloc(&d.cls_val, 4 * M);
+  rc |= s->alloc(&d.cls_cnt, 4 * M);
+  rc |= s->alloc(&s->cls_flags, 2);
   rc |= s->alloc(&d.gram, (int64_t)s->nb * B * B);
   rc |= s->alloc(&d.xgram, (int64_t)s->nb * B * B);
   rc |= s->alloc(&d.xgramT, (int64_t)s->nb * B * B);
@@ -1564,6 +1622,7 @@ int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
     case 104: *out = (double)s->fused.nsg; return 0;  // fused sweep: streaming workgroups (0 = per-block)
     case 105: *out = (double)s->fused.ccache; return 0;  // fused sweep: 2-bit code cache in LDS
     case 106: *out = (double)s->d.lag; return 0;  // pipeline lag
+    case 107: *out = (double)s->gram_np_init; return 0;  // Gram kernel: class planes of k_gram_int (0 = FP64 k_gram)
     case 110: case 111: case 112: case 113: case 114: case 115: case 116: case 117: case 118: case 119:
     case 120: case 121: case 122: case 123: case 124: case 125:
       *out = (double)sc.prof[which - 110]; return 0;
@@ -1595,6 +1654,8 @@ int brr_session_set_scalar(brr_session *s, int32_t which, double v) {
   return h2d(s, s->d.sc, &sc, 1);
 }
 
+static int64_t rc_or(int rc, int64_t n) { return rc ? rc : n; }
+
 int64_t brr_session_get_vector(brr_session *s, int32_t which, double *out) {
   if (!s) return -1;
   if (hipSetDevice(s->device) != hipSuccess) return -2;
@@ -1607,6 +1668,7 @@ int64_t brr_session_get_vector(brr_session *s, int32_t which, double *out) {
     case BRR_ALPHA: n = s->F; break;
     case 200: n = s->M; break;  // diagnostics: column sums of the device X (not in brr.h)
     case 201: n = (int64_t)s->nb * 16 + 9216; break;  // diagnostics: per-block event trace (brr_kernels.hip TR_*)
+    case 202: case 203: n = (int64_t)s->nb * s->B * s->B; break;  // diagnostics: the Gram / cross-Gram blocks
     default: set_error("unknown vector %d", which); return -1;
   }
   if (!out) return n;
@@ -1616,6 +1678,7 @@ int64_t brr_session_get_vector(brr_session *s, int32_t which, double *out) {
     for (int64_t i = 0; i < n; ++i) out[i] = (double)tr[(size_t)i];
     return n;
   }
+  if (which == 202 || which == 203) return (rc_or(d2h(s, out, which == 202 ? s->d.gram : s->d.xgram, n), n));
   if (which == 200) {
     std::vector<float> x((size_t)(s->d.ld * s->M));
     if (s->x2bit) {
