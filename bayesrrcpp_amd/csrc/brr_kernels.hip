@@ -1862,6 +1862,157 @@ __device__ __forceinline__ void chain_bayesr_resident(const Dev &d, int bs, doub
   }
 }
 
+// Serial chain, BayesR family, for blocks whose Gram block does not fit in LDS (B = 256, 512): lane
+// l holds positions l NS .. l NS + NS-1 with num and its decision window in registers; the Gram rows
+// are the raw rows of the positions predicted to change (static LDS slots, then the ring the idle
+// waves fill from HBM, else HBM itself), so an update is masked to the positions after the visited
+// one.  Each lane reads the constants of ITS lowest candidate (flags, D, noise, beta_old, slot) from
+// LDS and forms that candidate's new beta while the wave's ballot / owner-lane search runs, so a fast
+// step is ballot -> readlane of the owner's delta -> row update: the position's constants, the
+// division and the slot look-up are off the wave-uniform dependency chain (in the form it replaces,
+// four dependent LDS round trips and the division sat on it per step).  Operations and values are
+// those of that form (new beta = num / D + noise, BayesRv2.cpp:226-230).  Measured against it (C2,
+// same run, twice): sweeps 5-24 of a fresh chain 37.4 / 37.8 against 37.9 / 37.4 ms -- the burn-in
+// sweeps are bound by the solver's HBM round trips (Gram rows, corrections), not by this arithmetic.
+template <int B>
+__device__ __forceinline__ void chain_bayesr_rows(const Dev &d, int bs, double sigmaE, const double *Lr0,
+                                                  const double *Llo, const double *Lhi, double *Ldsel, double *Lsdz,
+                                                  const double *Lbo, double *Lbn, int *Lfl, int *Lks, const int *Lgi,
+                                                  const double *La, const double *Lden, const double *Lp,
+                                                  const double *Lx2, const double *Lz, const int *Lm, const int *Lslot,
+                                                  const int *Lspos, const double *slots, const double *Ggl, int RS,
+                                                  int nst, int nov, int *Lcons, int *Lready, bool prof) {
+#pragma clang fp contract(off)
+  constexpr int NS = B / 64;
+  constexpr uint32_t ALLQ = NS >= 32 ? 0xFFFFFFFFu : ((1u << NS) - 1u);
+  const int lane = threadIdx.x & 63;
+  double r[NS], lo[NS], hi[NS];
+  int gg[NS];
+  uint32_t act = 0, win = 0, valid = 0;
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    const int pos = lane * NS + q;
+    const bool in = pos < bs;
+    r[q] = in ? Lr0[pos] : 0.0;
+    lo[q] = in ? Llo[pos] : 1.0;
+    hi[q] = in ? Lhi[pos] : -1.0;
+    gg[q] = in ? Lgi[pos] : 0;
+    const int fl = in ? Lfl[pos] : 0;
+    const double tt = r[q] * r[q];
+    valid |= (uint32_t)in << q;
+    act |= (uint32_t)(in && (fl & PF_LIKELY)) << q;
+    win |= (uint32_t)(in && tt >= lo[q] && tt <= hi[q]) << q;
+  }
+  int nslow = 0, nsteps = 0, nref = 0, nglob = 0;
+  int kc = 0;  // ring cursor: entries below kc are released
+  uint64_t tref = 0;
+  const uint64_t tl0 = prof ? wall_clock64() : 0;
+  int i = 0;
+  while (i < bs) {
+    const int lowq = min(max(i - lane * NS, 0), NS);
+    const uint32_t ge = ALLQ & ~((1u << lowq) - 1u);
+    const uint32_t cand = valid & (act | ~win) & ge;
+    const int ql = cand ? __builtin_ctz(cand) : 0;
+    // this lane's lowest candidate: its constants and its new beta (the fast arm)
+    const int posl = min(lane * NS + ql, bs - 1);
+    const int fll = Lfl[posl];
+    const double dsl = Ldsel[posl], szl = Lsdz[posl], bol = Lbo[posl];
+    const int sll = Lslot[posl];
+    double rv = r[0];
+#pragma unroll
+    for (int q = 1; q < NS; ++q) rv = ql == q ? r[q] : rv;
+    const int ksl = fll & 0xFF;
+    const double bnl = ksl == 0 ? 0.0 : (ksl == FALLTHROUGH ? bol : rv / dsl + szl);  // BayesRv2.cpp:226-230
+    const int fastl = (int)((win >> ql) & 1u) & (int)((fll & PF_EX) == 0);
+    const uint64_t bal = __ballot(cand != 0);
+    if (!bal) break;  // the rest keep their decisions (no change)
+    const int L = __builtin_ctzll(bal);
+    const int qf = __builtin_amdgcn_readlane(ql, L);
+    const int first = L * NS + qf;  // wave-uniform
+    double delta;
+    if (__builtin_expect(__builtin_amdgcn_readlane(fastl, L) != 0, 1)) {
+      delta = readlane_f64(bnl - bol, L);
+      if (lane == L) Lbn[first] = bnl;
+    } else {
+      const double rf = readlane_f64(rv, L);
+      const bool exf = (__builtin_amdgcn_readlane(fll, L) & PF_EX) != 0;
+      if (!exf) {
+        // outside its window: re-decide `first` at its current num (wave-uniform), then re-examine it
+        const uint64_t tr0 = prof ? wall_clock64() : 0;
+        FastDec o = decide_pos_ool(d.gAssign, d.sigmaGG, d.pi, d.cva, d.G, d.K, rf, La + first, Lden + first, B, sigmaE,
+                                   Lp[first], Lx2[first], Lm[first]);
+        const double bo = Lbo[first];
+        const bool lk = o.ex || !(o.k == FALLTHROUGH || (o.k == 0 && bo == 0.0));
+        const double dsel = (!o.ex && o.k >= 1 && o.k != FALLTHROUGH) ? Lden[(o.k - 1) * B + first] : 1.0;
+        if (lane == 0) {
+          Lfl[first] = (o.k & 0xFF) | (o.ex ? PF_EX : 0) | (lk ? PF_LIKELY : 0);
+          Lks[first] = o.k;
+          Ldsel[first] = dsel;
+          Lsdz[first] = sqrt(sigmaE / dsel) * Lz[first];
+        }
+        if (lane == L) {
+#pragma unroll
+          for (int q = 0; q < NS; ++q)
+            if (q == qf) { lo[q] = o.lo; hi[q] = o.hi; }
+          act = (act & ~(1u << qf)) | ((uint32_t)lk << qf);
+          win = (win & ~(1u << qf)) | ((uint32_t)(!o.ex) << qf);
+        }
+        ++nref;
+        if (prof) tref += wall_clock64() - tr0;
+        continue;
+      }
+      const double bof = Lbo[first];
+      const int m = Lm[first];
+      const int g = d.gAssign ? d.gAssign[m] : 0;
+      Decision dc = decide_bayesr_ool(rf, Lx2[first], sigmaE, d.sigmaGG[g], d.pi + (int64_t)g * d.K, d.cva + g, d.G,
+                                      d.K, Lp[first], false);
+      const double bnf = dc.k == 0 ? 0.0 : (dc.k == FALLTHROUGH ? bof : rf / dc.denom + sqrt(sigmaE / dc.denom) * Lz[first]);
+      if (lane == 0) { Lbn[first] = bnf; Lks[first] = dc.k; }
+      delta = bnf - bof;
+      ++nslow;
+    }
+    if (delta != 0.0) {
+      // the visited position's Gram row: its static slot, its ring entry, or HBM
+      const int slf = __builtin_amdgcn_readlane(sll, L);
+      const double *grow = slf >= 0 ? slots + (int64_t)slf * B : Ggl + (int64_t)Lgi[first] * B;
+      bool from_ring = false;
+      if (slf < 0 && RS > 0) {  // predicted beyond the static slots: its ring entry
+        while (kc < nov && Lspos[nst + kc] < first) ++kc;  // entries passed without a change
+        if (kc < nov && Lspos[nst + kc] == first && ring_take(Lcons, Lready, RS, kc)) {
+          grow = slots + (int64_t)(nst + kc % RS) * B;
+          from_ring = true;
+        }
+      }
+      nglob += slf < 0 && !from_ring;
+#pragma unroll
+      for (int q = 0; q < NS; ++q) {
+        const int pos = lane * NS + q;
+        const bool later = pos > first && pos < bs;
+        const double gq = grow[gg[q]];
+        r[q] = later ? r[q] - gq * delta : r[q];
+        const double tt = r[q] * r[q];
+        const uint32_t bw = (uint32_t)(tt >= lo[q] && tt <= hi[q]);
+        win = later ? ((win & ~(1u << q)) | (bw << q)) : win;
+      }
+      if (from_ring) {
+        ++kc;
+        if (lane == 0) lds_st_rel(Lcons, kc);
+      }
+    }
+    i = first + 1;
+    ++nsteps;
+  }
+  if (lane == 0) lds_st_rel(Lcons, RING_DONE);
+  if (lane == 0 && nslow) atomicAdd(&d.sc->n_slow, (unsigned long long)nslow);
+  if (prof && lane == 0) {
+    atomicAdd(&d.sc->prof[6], (unsigned long long)nsteps);
+    atomicAdd(&d.sc->prof[7], (unsigned long long)nref);
+    atomicAdd(&d.sc->prof[4], (unsigned long long)nglob);
+    atomicAdd(&d.sc->prof[8], (unsigned long long)tref);
+    atomicAdd(&d.sc->prof[9], (unsigned long long)(wall_clock64() - tl0));
+  }
+}
+
 // The chains as separate (not inlined) functions: inside the persistent k_sweep the solver's
 // chain shares the register allocation of every role (256 VGPRs and several hundred spilled SGPRs
 // whose reloads land in the chain's loop); called, a chain gets its own allocation (Horseshoe:
@@ -2328,134 +2479,8 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     if (lane == 0) lds_st_rel(Lcons, RING_DONE);
     if (prof && lane == 0) atomicAdd(&d.sc->prof[6], (unsigned long long)bs);
   } else if (!HS && t < 64) {
-    double r[NS], lo[NS], hi[NS];
-    int gg[NS];
-    uint32_t act = 0, win = 0, valid = 0;
-#pragma unroll
-    for (int q = 0; q < NS; ++q) {
-      const int pos = lane * NS + q;
-      const bool in = pos < bs;
-      r[q] = in ? Lr0[pos] : 0.0;
-      lo[q] = in ? Llo[pos] : 1.0;
-      hi[q] = in ? Lhi[pos] : -1.0;
-      gg[q] = in ? Lgi[pos] : 0;
-      const int fl = in ? Lfl[pos] : 0;
-      const double tt = r[q] * r[q];
-      valid |= (uint32_t)in << q;
-      act |= (uint32_t)(in && (HS || (fl & PF_LIKELY))) << q;
-      win |= (uint32_t)(in && tt >= lo[q] && tt <= hi[q]) << q;
-    }
-    constexpr uint32_t ALL = NS >= 32 ? 0xFFFFFFFFu : ((1u << NS) - 1u);
-    const double *Ggl = d.gram + (int64_t)gb * B * B;
-    int nslow = 0, nsteps = 0, nref = 0, nglob = 0;
-    int kc = 0;  // ring cursor: entries below kc are released
-    uint64_t tref = 0, tcor = 0;
-    int i = 0;
-    while (i < bs) {
-      const int lowq = min(max(i - lane * NS, 0), NS);
-      const uint32_t ge = ALL & ~((1u << lowq) - 1u);
-      const uint32_t cand = valid & (act | ~win) & ge;
-      const uint64_t bal = __ballot(cand != 0);
-      if (!bal) break;  // the rest keep their decisions (no change)
-      const int L = __builtin_ctzll(bal);
-      const uint32_t cL = (uint32_t)__builtin_amdgcn_readlane((int)cand, L);
-      const int qf = __builtin_ctz(cL);
-      const int first = L * NS + qf;  // wave-uniform
-      double rv = r[0];
-#pragma unroll
-      for (int q = 1; q < NS; ++q)
-        if (qf == q) rv = r[q];
-      const double rf = readlane_f64(rv, L);
-      const int fl = Lfl[first];
-      const bool exf = (fl & PF_EX) != 0;
-      const bool winf = ((uint32_t)__builtin_amdgcn_readlane((int)win, L) >> qf) & 1u;
-      if (!HS && !exf && !winf) {
-        // re-decide `first` at its current num (wave-uniform), then re-examine it
-        const uint64_t tr0 = prof ? wall_clock64() : 0;
-        FastDec o = decide_pos_ool(d.gAssign, d.sigmaGG, d.pi, d.cva, d.G, d.K, rf, La + first, Lden + first, B, sigmaE, Lp[first], Lx2[first], Lm[first]);
-        const double bo = Lbo[first];
-        const bool lk = o.ex || !(o.k == FALLTHROUGH || (o.k == 0 && bo == 0.0));
-        const double dsel = (!o.ex && o.k >= 1 && o.k != FALLTHROUGH) ? Lden[(o.k - 1) * B + first] : 1.0;
-        if (lane == 0) {
-          Lfl[first] = (o.k & 0xFF) | (o.ex ? PF_EX : 0) | (lk ? PF_LIKELY : 0);
-          Lks[first] = o.k;
-          Ldsel[first] = dsel;
-          Lsdz[first] = sqrt(sigmaE / dsel) * Lz[first];
-        }
-        if (lane == L) {
-#pragma unroll
-          for (int q = 0; q < NS; ++q)
-            if (q == qf) { lo[q] = o.lo; hi[q] = o.hi; }
-          act = (act & ~(1u << qf)) | ((uint32_t)lk << qf);
-          win = (win & ~(1u << qf)) | ((uint32_t)(!o.ex) << qf);
-        }
-        ++nref;
-        if (prof) tref += wall_clock64() - tr0;
-        continue;
-      }
-      const double bof = Lbo[first];
-      double bn;
-      int ks;
-      if (HS) {
-        bn = rf / Ldsel[first] + Lsdz[first];  // HorseshoeR.cpp:234
-        ks = 1;
-      } else if (exf) {
-        const int m = Lm[first];
-        const int g = d.gAssign ? d.gAssign[m] : 0;
-        Decision dc = decide_bayesr_ool(rf, Lx2[first], sigmaE, d.sigmaGG[g], d.pi + (int64_t)g * d.K, d.cva + g, d.G,
-                                        d.K, Lp[first], false);
-        ks = dc.k;
-        bn = dc.k == 0 ? 0.0 : (dc.k == FALLTHROUGH ? bof : rf / dc.denom + sqrt(sigmaE / dc.denom) * Lz[first]);
-        ++nslow;
-      } else {
-        ks = fl & 0xFF;
-        bn = ks == 0 ? 0.0 : (ks == FALLTHROUGH ? bof : rf / Ldsel[first] + Lsdz[first]);  // BayesRv2.cpp:226-230
-      }
-      if (lane == 0) { Lbn[first] = bn; Lks[first] = ks; }
-      const double delta = bn - bof;
-      if (delta != 0.0) {
-        const uint64_t tc0 = prof ? wall_clock64() : 0;
-        const int sl = Lslot[first];
-        const double *grow = sl >= 0 ? slots + (int64_t)sl * B : Ggl + (int64_t)Lgi[first] * B;
-        bool from_ring = false;
-        if (sl < 0 && RS > 0) {  // predicted beyond the static slots: its ring entry
-          while (kc < nov && Lspos[nst + kc] < first) ++kc;  // entries passed without a change
-          if (kc < nov && Lspos[nst + kc] == first && ring_take(Lcons, Lready, RS, kc)) {
-            grow = slots + (int64_t)(nst + kc % RS) * B;
-            from_ring = true;
-          }
-        }
-        nglob += sl < 0 && !from_ring;
-        uint32_t w2 = win;
-#pragma unroll
-        for (int q = 0; q < NS; ++q) {
-          const int pos = lane * NS + q;
-          if (pos > first && pos < bs) {
-            r[q] = r[q] - grow[gg[q]] * delta;
-            const double tt = r[q] * r[q];
-            const uint32_t b = (uint32_t)(tt >= lo[q] && tt <= hi[q]);
-            w2 = (w2 & ~(1u << q)) | (b << q);
-          }
-        }
-        win = w2;
-        if (from_ring) {
-          ++kc;
-          if (lane == 0) lds_st_rel(Lcons, kc);
-        }
-        if (prof) tcor += wall_clock64() - tc0;
-      }
-      i = first + 1;
-      ++nsteps;
-    }
-    if (lane == 0) lds_st_rel(Lcons, RING_DONE);
-    if (lane == 0 && nslow) atomicAdd(&d.sc->n_slow, (unsigned long long)nslow);
-    if (prof && lane == 0) {
-      atomicAdd(&d.sc->prof[6], (unsigned long long)nsteps);
-      atomicAdd(&d.sc->prof[7], (unsigned long long)nref);
-      atomicAdd(&d.sc->prof[4], (unsigned long long)nglob);
-      atomicAdd(&d.sc->prof[8], (unsigned long long)tref);
-      atomicAdd(&d.sc->prof[9], (unsigned long long)tcor);
-    }
+    chain_bayesr_rows<B>(d, bs, sigmaE, Lr0, Llo, Lhi, Ldsel, Lsdz, Lbo, Lbn, Lfl, Lks, Lgi, La, Lden, Lp, Lx2, Lz, Lm,
+                         Lslot, Lspos, slots, d.gram + (int64_t)gb * B * B, RS, nst, nov, Lcons, Lready, prof);
   } else if (RS > 0 && nov > 0) {
     ring_produce<B, NW>(d.gram + (int64_t)gb * B * B, Lgi, Lspos, nst, nov, slots + (int64_t)nst * B, RS, Lcons,
                         Lready);

@@ -888,8 +888,13 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   // 90 sweeps/s at B = 128 / 512 -- so B = 128 below N = 32,768)
   // (row shards choose from the cohort's N_total: every shard must run the same B, and the same B
   // as the unsharded chain)
+  // (REFERENCE order recomputes its Gram blocks every sweep, 2 P B N class-pair products: C2 4.0
+  // against 1.8 sweeps/s at B = 128 / 512, profiles/r03_c2_reference_order_b*_intgram.log)
   int B = opt.block_size > 0 ? opt.block_size
-                             : ((model == MODEL_HORSESHOE || model == MODEL_GROUPS || N_total < 32768) ? 128 : 512);
+                             : ((model == MODEL_HORSESHOE || model == MODEL_GROUPS || N_total < 32768 ||
+                                 opt.order_mode == BRR_ORDER_REFERENCE)
+                                    ? 128
+                                    : 512);
   if (B % 64 != 0 || B > BMAX) { set_error("block_size=%d must be a multiple of 64 and <= %d", B, BMAX); return nullptr; }
   if (opt.shard_count < 1) opt.shard_count = 1;
   if (opt.shard_count > 1 && (col_offset % B) != 0) {
@@ -1081,8 +1086,18 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
       const double per_block = (ls ? atof(ls) : 9.0) * ((double)N / 1e5);
       d.lag_thresh = lg ? 1e300 : per_block * s->nb;  // (BRR_LAG: that lag in every sweep)
     }
+    // The streaming kernel's stream must never share a hardware queue with the session stream: a
+    // solver kernel ahead of it in the same queue would wait (bounded, census site 5) for streaming
+    // workgroups that cannot start.  HIP maps ordinary streams round-robin onto a small pool of
+    // queues (GPU_MAX_HW_QUEUES, 4 on the box), so two streams of one session can land on one
+    // queue once other streams come and go; a stream with a CU mask gets a queue of its own.
+    std::vector<uint32_t> cu_all((size_t)(cus + 31) / 32, 0xFFFFFFFFu);
+    if (s->fused.split && hipExtStreamCreateWithCUMask(&s->st_side, (uint32_t)cu_all.size(), cu_all.data()) != hipSuccess) {
+      (void)hipGetLastError();
+      s->st_side = nullptr;
+    }
     if (s->fused.split &&
-        (hipStreamCreateWithFlags(&s->st_side, hipStreamNonBlocking) != hipSuccess ||
+        ((!s->st_side && hipStreamCreateWithFlags(&s->st_side, hipStreamNonBlocking) != hipSuccess) ||
          hipEventCreateWithFlags(&s->ev_go, hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming) != hipSuccess)) {
       set_error("cannot create the streaming kernel's stream / events");

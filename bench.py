@@ -372,7 +372,8 @@ def main():
     N = args.N or cfg["N"]
     P = args.P or cfg["P"]
     model = {"v2": L.MODEL_V2, "groups": L.MODEL_GROUPS, "hs": L.MODEL_HORSESHOE}[cfg["model"]]
-    Bsz = args.block_size or (128 if model in (L.MODEL_HORSESHOE, L.MODEL_GROUPS) or N < 32768 else 512)  # = libbrr's automatic B
+    Bsz = args.block_size or (128 if model in (L.MODEL_HORSESHOE, L.MODEL_GROUPS) or N < 32768 or args.order == "reference"
+                              else 512)  # = libbrr's automatic B
     G = cfg["groups"]
     K = 1 if model == L.MODEL_HORSESHOE else len(CVA) + 1
     F = 1 if model == L.MODEL_GROUPS else 0

@@ -229,7 +229,7 @@ class Oracle:
         cfg.seed = seed
         cfg.order_mode = order_mode
         # 0 = the library's automatic block size (brr_session.cpp brr_session_create)
-        cfg.block_size = block_size or (128 if model in (HORSESHOE, GROUPS) or N < 32768 else 512)
+        cfg.block_size = block_size or (128 if model in (HORSESHOE, GROUPS) or N < 32768 or order_mode == ORDER_REFERENCE else 512)
         cfg.n_shards = n_shards
         cfg.shard_only = shard_only
         cfg.n_exchanges = n_exchanges
