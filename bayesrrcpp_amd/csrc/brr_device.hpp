@@ -118,6 +118,8 @@ struct Dev {
   int *cls_cnt;        // [M][4] real rows in each class
   int gram_np;         // k_gram_int's explicit class planes (1..3); 0 = the f64 matrix-core k_gram
   uint8_t *gram_codes; // k_gram_int's input: [nb][B/16][ldc][16] class codes of the current layout (k_encode_layout)
+  const uint8_t *xcodes; // f32 storage, BLOCKED order: the class codes in storage order (gram_codes of the
+                        // init layout), the source of the streamers' code cache (k_sweep_stream<2>), else nullptr
   const double *Y, *fixed, *cva;
   const int *gAssign;
   double *eps, *eps2, *eps_start, *deps, *beta, *xsq, *lambda, *hsv, *sigmaGG, *pi, *alpha;

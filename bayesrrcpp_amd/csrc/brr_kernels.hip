@@ -2890,10 +2890,12 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   // (a column's table: its 4 f32 values as doubles, read per value by code, so a product is the
   // f32 path's (double) x * e without a decode or conversion)
   auto lut_of = [&](int s) __attribute__((always_inline)) { return s_lut + (int64_t)(s % NLB) * B * 4; };
+  // XF = 2 (f32 storage, class-code cache): the class values play the value tables' part
+  const float *lutsrc = XF == 2 ? d.cls_val : d.xlut;
   auto stage_lut = [&](int s) __attribute__((always_inline)) {
     if constexpr (XF) {
       const int gb = d.gblk[s], bs = d.bsz[s];
-      const float4 *src = reinterpret_cast<const float4 *>(d.xlut) + (int64_t)gb * B;
+      const float4 *src = reinterpret_cast<const float4 *>(lutsrc) + (int64_t)gb * B;
       for (int i = t; i < B; i += SWEEP_NT) {
         const float4 l = i < bs ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
         double *dl = lut_of(s) + 4 * i;
@@ -2929,13 +2931,24 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   // loads into vector loads whose wait drains the prefetch ring.
   // f32: one float4 (4 rows) per column and lane; 2-bit: one 16-byte code group (16 columns x 4
   // rows) per lane in x[0]
-  using Raw = typename std::conditional<XF != 0, uint4, float4>::type;
-  constexpr int NR = XF ? 1 : CW;
+  // XF = 2: the item's CW float4 columns and, in x[CW], its 16-B class-code group (bits as a float4)
+  using Raw = typename std::conditional<XF == 1, uint4, float4>::type;
+  constexpr int NR = XF == 1 ? 1 : (XF == 2 ? CW + 1 : CW);
   auto issue = [&](int it, Raw (&x)[NR]) {
     const int s = sb0 + it / items, rem = it - (s - sb0) * items;
     const int c = rem / npass, p = rem - c * npass;
     const int64_t off = r0 + p * SROWS + 4 * lane < r1 ? r0 + p * SROWS + 4 * lane : r0;
-    if constexpr (XF) {
+    if constexpr (XF == 2) {
+      // storage order, as the 2-bit path: the block's 16 contiguous columns of this chunk (clamped
+      // to the last column in a short last block: those dots are never read) and their codes
+      static_assert(CW == 16, "an item is one 16-column code group");
+      const int64_t gb = d.gblk[s];  // wave-uniform
+      const int64_t c0 = gb * B + w * CPW + c * CW;
+#pragma unroll
+      for (int j = 0; j < CW; ++j) x[j] = ldg4(d.X + min(c0 + j, d.M - 1) * ld + off);
+      const uint4 cg = *reinterpret_cast<const uint4 *>(d.xcodes + ((c0 >> 4) * d.ldc + (off >> 2)) * 16);
+      x[CW] = make_float4(__uint_as_float(cg.x), __uint_as_float(cg.y), __uint_as_float(cg.z), __uint_as_float(cg.w));
+    } else if constexpr (XF) {
       static_assert(CW == 16, "a 2-bit item is one 16-column group");
       const int64_t gb = d.gblk[s];  // wave-uniform
       const int64_t grp = gb * (B >> 4) + ((w * CPW + c * CW) >> 4);
@@ -3000,7 +3013,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       apply_pending<XF>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, s_part,
                         (!XF && s + 1 < sb1) ? d.member + (int64_t)(s + 1) * B : nullptr, s_mem + ((s + 1) & 1) * B,
                         cache_of(a), s_mem,
-                        (XF && s + 1 < sb1) ? reinterpret_cast<const float4 *>(d.xlut) + (int64_t)d.gblk[s + 1] * B : nullptr,
+                        (XF && s + 1 < sb1) ? reinterpret_cast<const float4 *>(lutsrc) + (int64_t)d.gblk[s + 1] * B : nullptr,
                         lut_of(s + 1), lut_of(a), (XF && s + 1 < sb1) ? d.bsz[s + 1] : 0,
                         (prof && t == 0) ? acc_sub : nullptr);
       if (prof && t == 0) {
@@ -3019,16 +3032,22 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     const double e0 = e[0], e1 = e[1], e2 = e[2], e3 = e[3];
     if constexpr (XF) {
       // code cache: block s's tile of group w CPW / 16 + c at this lane's row quad p 64 + lane
+      uint4 cg;
+      if constexpr (XF == 2)
+        cg = make_uint4(__float_as_uint(xc[CW].x), __float_as_uint(xc[CW].y), __float_as_uint(xc[CW].z),
+                        __float_as_uint(xc[CW].w));
+      else
+        cg = xc[0];
       if (s_codes)
         reinterpret_cast<uint4 *>(s_codes)[((s % NCC) * (B >> 4) + ((w * CPW + c * CW) >> 4)) * (npass * 64) + p * 64 +
-                                           lane] = xc[0];
+                                           lane] = cg;
     }
     // one fused multiply-add per value into the column's accumulator, rows in order (the same
     // operations on the same f64 values for both storages: the chains are identical)
 #pragma unroll
     for (int j = 0; j < CW; ++j) {
       double x0, x1, x2, x3;
-      if constexpr (XF) {
+      if constexpr (XF == 1) {
         const uint32_t word = j < 4 ? xc[0].x : (j < 8 ? xc[0].y : (j < 12 ? xc[0].z : xc[0].w));
         const int sh = 8 * (j & 3);
         const double *lt = lut_of(s) + 4 * (w * CPW + c * CW + j);
@@ -3222,7 +3241,7 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
     // the code cache
     double *s_part = reinterpret_cast<double *>(s_mem + 2 * d.B);
     uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_part + SWEEP_NW * SROWS) : nullptr;
-    stream_role<STREAM_CW, XF ? STREAM_P2 : STREAM_P, XF>(d, (int)blockIdx.x - 1, rpw, npass, eps_l, s_pidx, s_pbo,
+    stream_role<STREAM_CW, XF == 1 ? STREAM_P2 : STREAM_P, XF>(d, (int)blockIdx.x - 1, rpw, npass, eps_l, s_pidx, s_pbo,
                                                          s_pbn, s_np, s_lut, s_mem, s_part, s_codes);
   }
 }
@@ -3271,7 +3290,7 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep_stream(Dev d, int nsg, in
   int *s_mem = s_pidx + (d.B + 16);
   double *s_part = reinterpret_cast<double *>(s_mem + 2 * d.B);
   uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_part + SWEEP_NW * SROWS) : nullptr;
-  stream_role<STREAM_CW, XF ? STREAM_P2 : STREAM_P, XF>(d, (int)blockIdx.x, rpw, npass, eps_l, s_pidx, s_pbo, s_pbn,
+  stream_role<STREAM_CW, XF == 1 ? STREAM_P2 : STREAM_P, XF>(d, (int)blockIdx.x, rpw, npass, eps_l, s_pidx, s_pbo, s_pbn,
                                                        s_np, s_lut, s_mem, s_part, s_codes);
 }
 
@@ -3648,12 +3667,16 @@ static const void *solve_kernel(int model, int B) {
   }
 }
 
-static const void *stream_kernel(bool xf) { return xf ? (const void *)k_sweep_stream<1> : (const void *)k_sweep_stream<0>; }
+// 0: f32 storage, 1: 2-bit codes, 2: f32 storage with the class-code cache (Dev::xcodes)
+static const void *stream_kernel(int xf) {
+  return xf == 1 ? (const void *)k_sweep_stream<1> : xf == 2 ? (const void *)k_sweep_stream<2> : (const void *)k_sweep_stream<0>;
+}
+static int stream_variant(const Dev &d, const FusedCfg &c) { return d.Xc ? 1 : (c.f32cc && d.xcodes) ? 2 : 0; }
 
 // streaming / reducing workgroups of the two-kernel sweep take more than half of a CU's LDS: one per CU
 constexpr size_t STREAM_LDS_MIN = SOLVE_LDS_MAX / 2 + 1024;
 
-bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
+bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) {
   // the 8 waves of a streaming workgroup split a block's columns in chunks of STREAM_CW
   if (cus < 3 || d.B % (SWEEP_NW * STREAM_CW) != 0) return false;
   // one CU each: the solver, nsg streamers (rows split evenly, at least 256 rows each) and
@@ -3678,7 +3701,7 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   const char *one = getenv("BRR_FUSED_SINGLE");
   const bool split = !(one && one[0] == '1');
   const void *fn = split ? solve_kernel(d.model, d.B) : sweep_kernel(d.model, d.B, xf);
-  const void *fst = split ? stream_kernel(xf) : nullptr;
+  const void *fst = split ? stream_kernel(xf ? 1 : 0) : nullptr;
   if (!fn) return false;
   hipFuncAttributes attr, attr_st;
   if (hipFuncGetAttributes(&attr, fn) != hipSuccess) return false;
@@ -3692,17 +3715,22 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   if ((size_t)nslot * d.B < solve_scratch_doubles(d.B, snt)) return false;
   // streamers: residual rows, [the value tables of two blocks], the change list (indices, old and
   // new betas), the member indices of two blocks in LDS
-  const size_t eps_bytes = (size_t)npass * SROWS * sizeof(double) + (xf ? (size_t)d.B * 32 * (d.lag + 3) : 0) +
-                           (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int)) + 2 * sizeof(int) * d.B +
-                           (size_t)SWEEP_NW * SROWS * sizeof(double);
-  const size_t code_bytes = xf ? (size_t)(d.lag + 2) * d.B * npass * 64 : 0;
+  // (f32 storage with a class-code cache: the value tables and code tiles as for 2-bit storage)
+  const bool tables = xf || (f32cc && split);
+  const size_t lut_bytes = (size_t)d.B * 32 * (d.lag + 3);
+  const size_t eps_base = (size_t)npass * SROWS * sizeof(double) + (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int)) +
+                          2 * sizeof(int) * d.B + (size_t)SWEEP_NW * SROWS * sizeof(double);
+  const size_t code_bytes = (size_t)(d.lag + 2) * d.B * npass * 64;
   const size_t st_budget = split ? SOLVE_LDS_MAX - attr_st.sharedSizeBytes : budget;
-  const bool ccache = xf && eps_bytes + code_bytes <= st_budget && !getenv("BRR_NO_CODE_CACHE");
-  const size_t st_lds = eps_bytes + (ccache ? code_bytes : 0);
+  const bool ccache = tables && eps_base + lut_bytes + code_bytes <= st_budget && !getenv("BRR_NO_CODE_CACHE");
+  const size_t st_lds = eps_base + (xf || ccache ? lut_bytes : 0) + (ccache ? code_bytes : 0);
   const size_t lds = split ? fixed + (size_t)nslot * 8 * d.B : std::max(fixed + (size_t)nslot * 8 * d.B, st_lds);
   if (lds > budget || st_lds > st_budget) return false;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) != hipSuccess) return false;
   if (split && hipFuncSetAttribute(fst, hipFuncAttributeMaxDynamicSharedMemorySize, (int)st_budget) != hipSuccess)
+    return false;
+  if (split && !xf && ccache &&
+      hipFuncSetAttribute(stream_kernel(2), hipFuncAttributeMaxDynamicSharedMemorySize, (int)st_budget) != hipSuccess)
     return false;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, snt, lds) != hipSuccess || per_cu < 1)
@@ -3723,7 +3751,8 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg) {
   cfg->ngroups = nred;
   cfg->nred = nred;
   cfg->lds = lds;
-  cfg->ccache = ccache ? 1 : 0;
+  cfg->ccache = (xf && ccache) ? 1 : 0;
+  cfg->f32cc = (!xf && ccache) ? 1 : 0;
   return true;
 }
 
@@ -3738,7 +3767,9 @@ hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipS
   if (c.split) {
     // the streaming kernel on the side stream, released by the same event that precedes the
     // solver on the session stream; the session stream waits for it before the next launch
-    const void *fs = solve_kernel(d.model, d.B), *ft = stream_kernel(d.Xc != nullptr);
+    const int xv = stream_variant(d, c);
+    const void *fs = solve_kernel(d.model, d.B), *ft = stream_kernel(xv);
+    if (xv == 2) cc = 1;  // (k_sweep_stream<2> always keeps the cache)
     if (!fs || !ft) return hipErrorInvalidValue;
     int total = nsg + 1 + nred;
     hipError_t e = hipEventRecord(ev_go, st);

@@ -37,12 +37,13 @@ hipError_t launch_group_sum(const GroupPtrs &p, int64_t n, hipStream_t st);
 hipError_t launch_prep(const Dev &d, uint32_t it, hipStream_t st);
 struct FusedCfg {
   int nsg = 0, rpw = 0, npass = 0, nslot = 0, ngroups = 0, nred = 0;
-  int ccache = 0;  // 2-bit storage: the streamers keep the last blocks' code tiles in LDS
+  int ccache = 0;  // the streamers keep the last blocks' code tiles in LDS (2-bit storage; f32: see f32cc)
+  int f32cc = 0;   // f32 storage: room for the class-code cache (used when Dev::xcodes is set: k_sweep_stream<2>)
   int split = 0;   // solver and streaming workgroups as two kernels side by side (else one k_sweep)
   size_t lds = 0;     // solver workgroup's dynamic LDS (one kernel: every workgroup's)
   size_t st_lds = 0;  // (split) streaming / reducing workgroups' dynamic LDS
 };
-bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg);
+bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc = false);
 // split: the solver kernel on st, the streaming kernel on st_side (ev_go / ev_done order them
 // against st); otherwise one cooperative k_sweep on st
 hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipStream_t st, hipStream_t st_side,

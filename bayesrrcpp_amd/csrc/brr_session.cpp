@@ -398,7 +398,7 @@ int do_sweep_local(brr_session *s) {
     Dev dp = d;
     dp.NG = s->fused.ngroups;
     dp.gtarget = s->fused.ngroups;
-    dp.slab_storage = d.Xc != nullptr;  // 2-bit streamers read blocks in storage order
+    dp.slab_storage = d.Xc != nullptr || d.xcodes != nullptr;  // streamers read blocks in storage order (2-bit, f32 code cache)
     if (s->timing) {
       const size_t i0 = s->ev_used;
       hipEvent_t e0 = s->ev(), e1 = s->ev();
@@ -605,7 +605,14 @@ int encode_layout(brr_session *s) {
 
 // BLOCKED / IDENTITY order: no Gram blocks after init, the class codes' memory is returned
 int release_gram_codes(brr_session *s) {
+  s->d.xcodes = nullptr;
   if (s->order_mode == BRR_ORDER_REFERENCE || !s->gram_codes) return 0;
+  if (s->fused.nsg > 0 && s->fused.f32cc && s->d.gram_np > 0 && s->order_mode == BRR_ORDER_BLOCKED) {
+    // f32 storage: the init layout's class codes are the storage-order codes the streamers' cache
+    // is filled from (k_sweep_stream<2>)
+    s->d.xcodes = s->gram_codes;
+    return 0;
+  }
   HIPCHK(hipStreamSynchronize(s->st));
   HIPCHK(hipFree(s->gram_codes));
   s->gram_codes = nullptr;
@@ -1073,7 +1080,14 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     // order (whole column blocks), but a REFERENCE block holds arbitrary columns -- the per-block
     // kernels read each member column by index
     const bool ref2bit = s->x2bit && s->order_mode == BRR_ORDER_REFERENCE;
-    if (rows || ref2bit || (pb && pb[0] == '1') || !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused))
+    // BRR_F32_CODE_CACHE=1: f32 storage in BLOCKED order keeps the streamed blocks' class codes in
+    // LDS (used when init finds every column class-coded) and applies the change lists from them
+    // instead of re-reading X.  Opt-in: it removes the apply's HBM re-read but not its time -- C4
+    // 13.42 against 13.87 sweeps/s (profiles/r03cc_c4*.log): the apply is bound by its LDS and
+    // issue work, not by HBM
+    const char *fcc = getenv("BRR_F32_CODE_CACHE");
+    const bool f32cc = !s->x2bit && s->order_mode == BRR_ORDER_BLOCKED && fcc && fcc[0] == '1';
+    if (rows || ref2bit || (pb && pb[0] == '1') || !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused, f32cc))
       s->fused = FusedCfg{};
     if (s->fused.nsg == 0) d.lag = 1;
     // lag 1 while the solver bounds the sweep: more than ~9 changed markers per block at C2's
@@ -1635,7 +1649,7 @@ int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
     case 101: *out = (double)sc.n_changed; return 0;
     case 102: *out = (double)sc.prof_on; return 0;
     case 104: *out = (double)s->fused.nsg; return 0;  // fused sweep: streaming workgroups (0 = per-block)
-    case 105: *out = (double)s->fused.ccache; return 0;  // fused sweep: 2-bit code cache in LDS
+    case 105: *out = (double)(s->fused.ccache || s->d.xcodes != nullptr); return 0;  // fused sweep: code cache in LDS
     case 106: *out = (double)s->d.lag; return 0;  // pipeline lag
     case 107: *out = (double)s->gram_np_init; return 0;  // Gram kernel: class planes of k_gram_int (0 = FP64 k_gram)
     case 110: case 111: case 112: case 113: case 114: case 115: case 116: case 117: case 118: case 119:

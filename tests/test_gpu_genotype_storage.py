@@ -201,3 +201,27 @@ def test_2bit_code_cache_midsize(brr, require_gpu, monkeypatch, model, cap):
             s.sweep(1)
         _identical(a, b, L, model, f"cache model={model} cap={cap} it={it}")
         _identical(a, c, L, model, f"no cache model={model} cap={cap} it={it}")
+
+
+@pytest.mark.parametrize("model", [1, 3])
+def test_f32_class_code_cache_identical(brr, oracle_mod, require_gpu, model, monkeypatch):
+    """f32 storage with every column class-coded (BLOCKED order, B = 128, BRR_F32_CODE_CACHE=1): the streamers keep the
+    streamed blocks' class codes in LDS and apply the change lists from them (k_sweep_stream<2>)
+    instead of re-reading X.  Same values in the same order: the chain equals the f32 chain without
+    the cache bit for bit, and the oracle within the parity tolerance."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P = 1003, 1100
+    X, Y, _ = O.synth_cohort(20261015, N, P, h2=0.5, n_causal=40)
+    G = 4 if model == L.MODEL_GROUPS else 1
+    gA = (np.arange(P) * G // P).astype(np.int32) if G > 1 else None
+    monkeypatch.setenv("BRR_F32_CODE_CACHE", "1")
+    a = _session(brr, L, model, X, Y, 128, L.X_F32, G, gA)
+    assert a.scalar(105) == 1 and a.scalar(104) > 0, "f32 code cache not in use"
+    monkeypatch.delenv("BRR_F32_CODE_CACHE")
+    b = _session(brr, L, model, X, Y, 128, L.X_F32, G, gA)
+    assert b.scalar(105) == 0
+    for it in range(4):
+        a.sweep(1)
+        b.sweep(1)
+        _identical(a, b, L, model, f"model={model} it={it}")
