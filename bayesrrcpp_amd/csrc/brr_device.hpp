@@ -59,7 +59,8 @@ struct Scal {
   unsigned long long nch_mark;   // n_changed at the end of the previous sweep
   int prof_on;                   // diagnostics: k_solve phase timers on
   int pad2;
-  unsigned long long prof[16];   // k_solve phase totals (wall_clock64 ticks, 100 MHz), counters
+  unsigned long long prof[20];   // k_solve phase totals (wall_clock64 ticks, 100 MHz), counters;
+                                 // [16]: streamer boundaries served by the list prefetch
 };
 
 struct Hyper {

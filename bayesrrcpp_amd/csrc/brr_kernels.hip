@@ -2864,6 +2864,90 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
   if (ptime) ptime[3] += wall_clock64() - tq4;
 }
 
+// The part (pass, entry range) of a change list of np entries that wave w applies (apply_pending's
+// split; one pass per wave when npass <= 8, the case the prefetch serves).
+struct ApplyPart {
+  int p0, e0, e1;
+};
+__device__ __forceinline__ ApplyPart apply_part(int np, int npass, int w) {
+  const int G = npass >= SWEEP_NW ? 1 : SWEEP_NW / npass;
+  const int p0 = G == 1 ? w : w % npass, part = G == 1 ? 0 : w / npass;
+  return {p0, part < G ? (np * part / G) : np, part < G ? (np * (part + 1) / G) : np};
+}
+
+// apply_pending for f32 storage when every wave of the workgroup prefetched the list during the
+// previous block (stream_role's list prefetch): the list (np entries, nr real, lane e's
+// b_old - b_new in lpd) is in registers and this wave's part of the columns' rows is in LDS
+// (stage[(e npass + p) 256 + row], 16-B LDS-DMA of exactly the loads apply_pending would issue),
+// so the boundary makes no HBM round trip.  Same parts, entry order and operations as
+// apply_pending: the residual is bit-identical (the neutral padding entries, whose products are
+// exact zeros, are skipped).  npass <= 8.
+__device__ __forceinline__ void apply_staged(const Dev &d, int np, int nr, double lpd, int64_t r0, int64_t r1,
+                                             int npass, double *eps_l, double *s_part, const float *stage,
+                                             const int *msrc, int *mdst, uint64_t *ptime) {
+#pragma clang fp contract(off)
+  const uint64_t tq0 = ptime ? wall_clock64() : 0;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const bool mcopy = msrc != nullptr && t < d.B;
+  const int mval = mcopy ? msrc[t] : 0;
+  const int G = npass >= SWEEP_NW ? 1 : SWEEP_NW / npass;
+  const int ldp = npass * SROWS;
+  if (np > 0) {
+    const ApplyPart ap = apply_part(np, npass, w);
+    const int part = G == 1 ? 0 : w / npass;
+    if (ap.p0 < npass && ap.e0 < ap.e1) {
+      const int off = ap.p0 * SROWS + 4 * lane;
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      const int ee = min(ap.e1, nr);
+      for (int e = ap.e0; e < ee; ++e) {
+        const double dd = readlane_f64(lpd, e);
+        const float4 x = *reinterpret_cast<const float4 *>(stage + ((int64_t)e * npass + ap.p0) * SROWS + 4 * lane);
+        a0 = __builtin_fma((double)x.x, dd, a0);
+        a1 = __builtin_fma((double)x.y, dd, a1);
+        a2 = __builtin_fma((double)x.z, dd, a2);
+        a3 = __builtin_fma((double)x.w, dd, a3);
+      }
+      if (G == 1) {
+        if (r0 + off < r1) {
+          double *ep = eps_l + off;
+          ep[0] = ep[0] + a0;
+          ep[1] = ep[1] + a1;
+          ep[2] = ep[2] + a2;
+          ep[3] = ep[3] + a3;
+        }
+      } else {
+        double *pp = s_part + (int64_t)part * ldp + off;
+        pp[0] = a0;
+        pp[1] = a1;
+        pp[2] = a2;
+        pp[3] = a3;
+      }
+    }
+    const uint64_t tq2 = ptime ? wall_clock64() : 0;
+    if (ptime) ptime[1] += tq2 - tq0;
+    if (G > 1) {
+      for (int i = t; i < G * ldp; i += SWEEP_NT) {
+        const int pt = i / ldp;
+        if (np * pt / G == np * (pt + 1) / G) s_part[i] = 0.0;
+      }
+      __syncthreads();
+      if (ptime) ptime[2] += wall_clock64() - tq2;
+      for (int i = t; i < ldp; i += SWEEP_NT) {
+        if (r0 + i < r1) {
+          double acc = s_part[i];
+          for (int pt = 1; pt < G; ++pt) acc += s_part[pt * ldp + i];
+          eps_l[i] = eps_l[i] + acc;
+        }
+      }
+    }
+  }
+  const uint64_t tq4 = ptime ? wall_clock64() : 0;
+  if (mcopy) mdst[t] = mval;
+  __syncthreads();
+  if (ptime) ptime[3] += wall_clock64() - tq4;
+}
+
 // XF = 1: 2-bit genotype codes in tiles (brr_device.hpp).  A block is streamed in STORAGE order:
 // item (chunk c of wave w, pass p) = the block's 16-column group w CPW / 16 + c and this lane's row
 // quad, ONE 16-byte load per lane (1 KiB per wave instruction, 16 columns x 256 rows), so the
@@ -2874,10 +2958,12 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
 template <int CW, int P, int XF>
 __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int npass, double *eps_l, int *s_pidx,
                                             double *s_pbo, double *s_pbn, int *s_np, double *s_lut, int *s_mem,
-                                            double *s_part, uint8_t *s_codes) {
+                                            double *s_part, uint8_t *s_codes, int pfe = 0, int *s_pf = nullptr,
+                                            float *s_stage = nullptr) {
 #pragma clang fp contract(off)
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  if (!XF && pfe > 0 && lane == 0) s_pf[w] = -1;  // (before the first barrier below)
   const int64_t r0 = (int64_t)g * rpw, r1 = min((int64_t)d.N, r0 + rpw);
   const int B = d.B, nb = d.nb;
   const int64_t ld = d.ld;
@@ -2978,11 +3064,54 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   // diagnostics (prof): this workgroup's accumulated wait / apply / streaming time of the sweep
   uint64_t acc_wait = 0, acc_apply = 0, acc_stream = 0, t_mark = prof ? wall_clock64() : 0;
   uint64_t acc_sub[4] = {0, 0, 0, 0};  // apply: list staging, products, part barrier, staging stores (ptime)
-  // Item it: s = it / items (block), rem = position in the block; c = chunk, p = pass.
-  // boundary(s): block s's start (staging, or the apply of block s-1-LAG's changes);
-  // consume(it, xc): this item's dot contributions from its loaded data xc, and the wave reduction
-  // at a chunk's last pass; block_end(it, s, xn): the prefetch into xn issued after the partial-dot
-  // stores, their drain and the group-counter arrival.
+  // List prefetch (f32 storage, pfe > 0).  While block s streams, each wave fetches the change
+  // list that boundary s + 1 applies (block s - LAG; with lag 2 the solver has usually published it
+  // before block s starts) one step per item, so no step waits on memory: poll the solver's
+  // counter, load the count and lane e's entry e, then LDS-DMA its own part's columns (16 B per
+  // lane, the loads apply_pending would issue) and flag it in s_pf[w].  A list longer than pfe,
+  // or one not yet published when block s ends, is applied the ordinary way.
+  // Three VGPRs of state: pf_m (the counter, then lane e < 32: entry e's column, lane 62 / 63: the
+  // padded / real length) and pf_d (lane e < 32: b_old, lane 32 + e: b_new; then lane e: the delta).
+  int pf_st = 0;  // 0 poll next, 1 poll in flight, 2 list in flight, 3 staged, 4 too long
+  int pf_m = 0, pf_np = 0, pf_nr = 0;
+  double pf_d = 0.0;
+  auto pf_step = [&](int s) __attribute__((always_inline)) {
+    if constexpr (!XF) {
+      const int a = s - LAG;  // the list boundary s + 1 applies
+      if (pfe == 0 || pf_st >= 3 || s + 1 >= sb1 || a < sb0) return;
+      const int slot = a % NSLOT;
+      if (pf_st == 2) {
+        pf_np = __builtin_amdgcn_readlane(pf_m, 62);
+        pf_nr = __builtin_amdgcn_readlane(pf_m, 63);
+        if (pf_nr > pfe || pf_np > 48) { pf_st = 4; return; }
+        pf_d = pf_d - __shfl(pf_d, (lane + 32) & 63);  // lane e < 32: b_old - b_new
+        const ApplyPart ap = apply_part(pf_np, npass, w);
+        if (ap.p0 < npass) {
+          const int64_t off = r0 + ap.p0 * SROWS + 4 * lane < r1 ? r0 + ap.p0 * SROWS + 4 * lane : r0;
+          const int ee = min(ap.e1, pf_nr);
+          for (int e = ap.e0; e < ee; ++e) {
+            const int64_t col = __builtin_amdgcn_readlane(pf_m, e);
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(d.X + col * ld + off),
+                (__attribute__((address_space(3))) void *)(s_stage + ((int64_t)e * npass + ap.p0) * SROWS), 16, 0, 0);
+          }
+        }
+        pf_st = 3;
+        if (lane == 0) s_pf[w] = a;  // read at boundary s + 1, after block s's closing barrier
+        return;
+      }
+      if (pf_st == 1 && (int)((unsigned)__builtin_amdgcn_readfirstlane(pf_m) - (unsigned)(d.sbase + a + 1)) >= 0) {
+        // (entries past nr are the neutral padding; lanes 32..61 load an unused word)
+        const int *pidx = d.pend_idx + slot * d.pend_stride;
+        pf_m = ld_sc1_int(lane < 32 ? pidx + lane : lane == 62 ? d.pend_n + slot : lane == 63 ? d.pend_n + NSLOT + slot : pidx);
+        pf_d = ld_sc1(lane < 32 ? d.pend_bo + slot * d.pend_stride + lane : d.pend_bn + slot * d.pend_stride + (lane - 32));
+        pf_st = 2;
+        return;
+      }
+      pf_m = ld_sc1_int(d.sync + SY_PEND);
+      pf_st = 1;
+    }
+  };
   auto boundary = [&](int s) __attribute__((always_inline)) {
     const int sr = s - sb0;  // position in this launch
     if (sr >= 1 && sr <= LAG) {
@@ -3000,6 +3129,35 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       // then hold every change before block s-1, which the solver corrects for through the
       // cross-Gram; lag 2: before block s-2, corrected for blocks s-2 and s-1)
       const int a = s - 1 - LAG;
+      // every wave prefetched list a during block s-1 (pf_step; its flags were stored before the
+      // barrier that ended block s-1): no wait, no list staging, the columns' rows are in LDS
+      bool fast = false;
+      if constexpr (!XF) {
+        if (pfe > 0) {
+          fast = true;
+#pragma unroll
+          for (int q = 0; q < SWEEP_NW; ++q) fast = fast && s_pf[q] == a;
+        }
+      }
+      pf_st = 0;
+      if (fast) {
+        if (prof && t == 0) {
+          const uint64_t tn = wall_clock64();
+          acc_wait += tn - t_mark;
+          t_mark = tn;
+        }
+        apply_staged(d, pf_np, pf_nr, pf_d,
+                     r0, r1, npass, eps_l, s_part, s_stage,
+                     s + 1 < sb1 ? d.member + (int64_t)(s + 1) * B : nullptr, s_mem + ((s + 1) & 1) * B,
+                     (prof && t == 0) ? acc_sub : nullptr);
+        if (prof && t == 0) {
+          const uint64_t tn = wall_clock64();
+          acc_apply += tn - t_mark;
+          t_mark = tn;
+          atomicAdd(&d.sc->prof[16], 1ull);  // boundaries served by the prefetch
+        }
+        return;
+      }
       if (t == 0) {
         wait_geq(d.sync + SY_PEND, d.sbase + a + 1, d.sync, 2);
         if (prof) {
@@ -3119,6 +3277,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
         const bool blk_end = u == R - 1 && rem == items - 1;
         if (!blk_end) issue(min(it + P, total - 1), xq[(u + P) % R]);
         consume(it, xq[u]);
+        pf_step(s);
         if constexpr (u == R - 1)
           if (blk_end) block_end(it, s, xq[(u + P) % R], true);
       });
@@ -3133,6 +3292,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       // last item the prefetch is issued after the partial-dot stores instead (block_end)
       if (!blk_end && it + P < total) issue(it + P, xq[P]);
       consume(it, xq[0]);
+      pf_step(s);
 #pragma unroll
       for (int q = 0; q < P; ++q)
 #pragma unroll
@@ -3274,10 +3434,12 @@ __global__ __launch_bounds__(SOLVE_NT, 1) void k_sweep_solve(Dev d, uint32_t it,
 }
 
 template <int XF>
-__global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep_stream(Dev d, int nsg, int rpw, int npass, int nred, int ccache) {
+__global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep_stream(Dev d, int nsg, int rpw, int npass, int nred, int ccache,
+                                                               int pfe) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_np[2];
   __shared__ int s_ok;
+  __shared__ int s_pf[SWEEP_NW];
   if (!sweep_census(d, nsg + 1 + nred, &s_ok)) return;
   if ((int)blockIdx.x >= nsg) {
     reduce_role(d, (int)blockIdx.x - nsg, nsg, nred, d.sc->prof_on);
@@ -3290,8 +3452,11 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep_stream(Dev d, int nsg, in
   int *s_mem = s_pidx + (d.B + 16);
   double *s_part = reinterpret_cast<double *>(s_mem + 2 * d.B);
   uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_part + SWEEP_NW * SROWS) : nullptr;
+  // (f32 storage) the list prefetch's staging area: pfe entries x npass passes x 1 KiB
+  float *s_stage = reinterpret_cast<float *>(s_part + SWEEP_NW * SROWS);
   stream_role<STREAM_CW, XF == 1 ? STREAM_P2 : STREAM_P, XF>(d, (int)blockIdx.x, rpw, npass, eps_l, s_pidx, s_pbo, s_pbn,
-                                                       s_np, s_lut, s_mem, s_part, s_codes);
+                                                       s_np, s_lut, s_mem, s_part, s_codes, XF ? 0 : pfe, s_pf,
+                                                       s_stage);
 }
 
 // ------------------------------------------------------------------------------------
@@ -3724,6 +3889,14 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
   const size_t st_budget = split ? SOLVE_LDS_MAX - attr_st.sharedSizeBytes : budget;
   const bool ccache = tables && eps_base + lut_bytes + code_bytes <= st_budget && !getenv("BRR_NO_CODE_CACHE");
   const size_t st_lds = eps_base + (xf || ccache ? lut_bytes : 0) + (ccache ? code_bytes : 0);
+  // (split, f32 storage) the list prefetch's staging area in the room left: up to 32 entries of
+  // npass KiB, when every wave has at most one pass (BRR_LIST_PREFETCH=0: off)
+  int pfe = 0;
+  if (split && !xf && npass <= SWEEP_NW && !(getenv("BRR_LIST_PREFETCH") && getenv("BRR_LIST_PREFETCH")[0] == '0')) {
+    const size_t room = st_budget > st_lds ? st_budget - st_lds : 0;
+    pfe = (int)std::min<size_t>(32, room / ((size_t)npass * SROWS * sizeof(float))) / 16 * 16;
+  }
+  const size_t st_lds_pf = st_lds + (size_t)pfe * npass * SROWS * sizeof(float);
   const size_t lds = split ? fixed + (size_t)nslot * 8 * d.B : std::max(fixed + (size_t)nslot * 8 * d.B, st_lds);
   if (lds > budget || st_lds > st_budget) return false;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) != hipSuccess) return false;
@@ -3737,7 +3910,8 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
     return false;
   cfg->split = split ? 1 : 0;
   // (split) the streaming kernel's LDS request: padded past half a CU's LDS, one workgroup per CU
-  cfg->st_lds = split ? std::min(st_budget, std::max(st_lds, STREAM_LDS_MIN - attr_st.sharedSizeBytes)) : 0;
+  cfg->st_lds = split ? std::min(st_budget, std::max(st_lds_pf, STREAM_LDS_MIN - attr_st.sharedSizeBytes)) : 0;
+  cfg->pfe = pfe;
   if (split) {
     per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fst, SWEEP_NT, cfg->st_lds) != hipSuccess || per_cu != 1)
@@ -3776,7 +3950,8 @@ hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipS
     if (e == hipSuccess) e = hipStreamWaitEvent(st_side, ev_go, 0);
     void *sargs[] = {&dd, &it, &nslot, &total};
     if (e == hipSuccess) e = hipLaunchKernel(fs, dim3(1), dim3(SOLVE_NT), sargs, (unsigned)c.lds, st);
-    void *targs[] = {&dd, &nsg, &rpw, &npass, &nred, &cc};
+    int pfe = xv == 0 ? c.pfe : 0;
+    void *targs[] = {&dd, &nsg, &rpw, &npass, &nred, &cc, &pfe};
     if (e == hipSuccess)
       e = hipLaunchKernel(ft, dim3((unsigned)(nsg + nred)), dim3(SWEEP_NT), targs, (unsigned)c.st_lds, st_side);
     if (e == hipSuccess) e = hipEventRecord(ev_done, st_side);

@@ -1653,7 +1653,7 @@ int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
     case 106: *out = (double)s->d.lag; return 0;  // pipeline lag
     case 107: *out = (double)s->gram_np_init; return 0;  // Gram kernel: class planes of k_gram_int (0 = FP64 k_gram)
     case 110: case 111: case 112: case 113: case 114: case 115: case 116: case 117: case 118: case 119:
-    case 120: case 121: case 122: case 123: case 124: case 125:
+    case 120: case 121: case 122: case 123: case 124: case 125: case 126: case 127: case 128: case 129:
       *out = (double)sc.prof[which - 110]; return 0;
     default: set_error("unknown scalar %d", which); return -1;
   }

@@ -546,6 +546,10 @@ def main():
         diag["solve_chain_clock_ghz"] = round(s.scalar(121) / max(1.0, s.scalar(112)) * 0.1, 3)
         # serial chain loop alone (shader clocks per chain step; wave 0 of the solver)
         diag["solve_chain_loop_cycles_per_step"] = round(s.scalar(122) / max(1.0, s.scalar(116)), 1)
+        # streamer boundaries whose change list was prefetched (per streaming workgroup and block)
+        nsg_ = int(s.scalar(104))
+        if nsg_ > 0:
+            diag["list_prefetch_frac"] = round(s.scalar(126) / (2.0 * nsg_ * max(1, -(-P // Bsz))), 3)
         if int(s.scalar(104)) > 0:
             # per-block event trace of one fused sweep (brr_kernels.hip TR_*), medians in us
             s.set_scalar(102, 1.0)
