@@ -2660,6 +2660,16 @@ constexpr int FUSED_GROUP = FUSED_GROUP_N;
 #ifndef BRR_APPLY_AB
 #define BRR_APPLY_AB 4
 #endif
+// Parts of a change list of np entries (padded length): a list of at most 16 entries -- the steady
+// state's, a few real ones plus padding -- is applied by one wave per pass (no cross-wave sum and
+// its barrier); a longer one in SWEEP_NW / npass parts per pass.  Every path applies a list the same
+// way, so the residual does not depend on the storage or on whether the list was prefetched.
+#ifndef BRR_APPLY_SMALL
+#define BRR_APPLY_SMALL 16
+#endif
+__device__ __forceinline__ int apply_nparts(int np, int npass) {
+  return (npass >= SWEEP_NW || np <= BRR_APPLY_SMALL) ? 1 : SWEEP_NW / npass;
+}
 template <int XF>
 __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0, int64_t r1, int npass,
                                               double *eps_l, int *s_pidx, double *s_pbo, double *s_pbn,
@@ -2723,17 +2733,20 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
       }
       s_pd[e] = ld_sc1(pbo + e) - ld_sc1(pbn + e);
     }
-    if (lane == 0) s_np[0] = np;
+    if (lane == 0) { s_np[0] = np; s_np[1] = nr; }
   }
   __syncthreads();
   const int np = __builtin_amdgcn_readfirstlane(s_np[0]);
+  const int nr = __builtin_amdgcn_readfirstlane(s_np[1]);
   const uint64_t tq1 = ptime ? wall_clock64() : 0;
-  const int G = npass >= SWEEP_NW ? 1 : SWEEP_NW / npass;  // parts of the list
+  const int G = apply_nparts(np, npass);  // parts of the list
   const int ldp = npass * SROWS;                          // doubles per part in s_part
   if (np > 0) {
     const int p0 = G == 1 ? w : w % npass, part = G == 1 ? 0 : w / npass;
     const int pstep = G == 1 ? SWEEP_NW : npass;  // (G > 1: one pass per wave)
     const int e0 = part < G ? (np * part / G) : np, e1 = part < G ? (np * (part + 1) / G) : np;
+    // the part's real entries: the neutral padding's products are exact zeros and are skipped
+    const int ee = min(e1, nr);
     for (int p = p0; p < npass && e0 < e1; p += pstep) {
       const int off = p * SROWS + 4 * lane;  // this lane's 4 rows, relative to r0
       const bool ok = r0 + off < r1;
@@ -2758,7 +2771,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
           auto consume = [&](const uint32_t (&r)[AB], int e) __attribute__((always_inline)) {
 #pragma unroll
             for (int q = 0; q < AB; ++q) {
-              if (e + q < e1) {
+              if (e + q < ee) {
                 const double *lt = lutb + 4 * s_ppos[e + q];
                 const uint32_t b = r[q];
                 const double dd = s_pd[e + q];
@@ -2769,19 +2782,20 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
               }
             }
           };
+          if (e0 >= ee) return;
 #pragma unroll
-          for (int q = 0; q < AB; ++q) ra[q] = rload(min(e0 + q, e1 - 1));
-          for (int e = e0; e < e1; e += 2 * AB) {
-            const bool more = e + AB < e1;
+          for (int q = 0; q < AB; ++q) ra[q] = rload(min(e0 + q, ee - 1));
+          for (int e = e0; e < ee; e += 2 * AB) {
+            const bool more = e + AB < ee;
             if (more) {
 #pragma unroll
-              for (int q = 0; q < AB; ++q) rb[q] = rload(min(e + AB + q, e1 - 1));
+              for (int q = 0; q < AB; ++q) rb[q] = rload(min(e + AB + q, ee - 1));
             }
             consume(ra, e);
             if (!more) break;
-            if (e + 2 * AB < e1) {
+            if (e + 2 * AB < ee) {
 #pragma unroll
-              for (int q = 0; q < AB; ++q) ra[q] = rload(min(e + 2 * AB + q, e1 - 1));
+              for (int q = 0; q < AB; ++q) ra[q] = rload(min(e + 2 * AB + q, ee - 1));
             }
             consume(rb, e + AB);
           }
@@ -2793,7 +2807,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
       auto consume = [&](const float4 (&x)[AB], int e) __attribute__((always_inline)) {
 #pragma unroll
         for (int q = 0; q < AB; ++q) {
-          if (e + q < e1) {
+          if (e + q < ee) {
             const double dd = s_pd[e + q];  // (fused multiply-add, as the 2-bit path)
             a0 = __builtin_fma((double)x[q].x, dd, a0);
             a1 = __builtin_fma((double)x[q].y, dd, a1);
@@ -2802,21 +2816,23 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
           }
         }
       };
+      if (e0 < ee) {
 #pragma unroll
-      for (int q = 0; q < AB; ++q) xa[q] = xload(min(e0 + q, e1 - 1));
-      for (int e = e0; e < e1; e += 2 * AB) {
-        const bool more = e + AB < e1;
+      for (int q = 0; q < AB; ++q) xa[q] = xload(min(e0 + q, ee - 1));
+      for (int e = e0; e < ee; e += 2 * AB) {
+        const bool more = e + AB < ee;
         if (more) {
 #pragma unroll
-          for (int q = 0; q < AB; ++q) xb[q] = xload(min(e + AB + q, e1 - 1));
+          for (int q = 0; q < AB; ++q) xb[q] = xload(min(e + AB + q, ee - 1));
         }
         consume(xa, e);
         if (!more) break;
-        if (e + 2 * AB < e1) {
+        if (e + 2 * AB < ee) {
 #pragma unroll
-          for (int q = 0; q < AB; ++q) xa[q] = xload(min(e + 2 * AB + q, e1 - 1));
+          for (int q = 0; q < AB; ++q) xa[q] = xload(min(e + 2 * AB + q, ee - 1));
         }
         consume(xb, e + AB);
+      }
       }
       }
       if (G == 1) {
@@ -2870,7 +2886,7 @@ struct ApplyPart {
   int p0, e0, e1;
 };
 __device__ __forceinline__ ApplyPart apply_part(int np, int npass, int w) {
-  const int G = npass >= SWEEP_NW ? 1 : SWEEP_NW / npass;
+  const int G = apply_nparts(np, npass);
   const int p0 = G == 1 ? w : w % npass, part = G == 1 ? 0 : w / npass;
   return {p0, part < G ? (np * part / G) : np, part < G ? (np * (part + 1) / G) : np};
 }
@@ -2891,7 +2907,7 @@ __device__ __forceinline__ void apply_staged(const Dev &d, int np, int nr, doubl
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const bool mcopy = msrc != nullptr && t < d.B;
   const int mval = mcopy ? msrc[t] : 0;
-  const int G = npass >= SWEEP_NW ? 1 : SWEEP_NW / npass;
+  const int G = apply_nparts(np, npass);
   const int ldp = npass * SROWS;
   if (np > 0) {
     const ApplyPart ap = apply_part(np, npass, w);
