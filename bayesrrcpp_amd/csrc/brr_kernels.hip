@@ -1540,6 +1540,27 @@ __device__ __forceinline__ float4 ldg4(const float *p) {
   const v4f v = *(const __attribute__((address_space(1))) v4f *)(p);
   return make_float4(v.x, v.y, v.z, v.w);
 }
+// The streamers' X / code-tile loads: every byte is read once per sweep and the shard is far larger
+// than the Infinity Cache, so they carry the non-temporal hint (MI355X_MICROARCH.md "nt-weights":
+// bytes streamed once; BRR_STREAM_NT=0 builds the default policy for comparison)
+#ifndef BRR_STREAM_NT
+#define BRR_STREAM_NT 1
+#endif
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldg4_stream(const float *p) {
+#if BRR_STREAM_NT
+  const v4f v = __builtin_nontemporal_load((const __attribute__((address_space(1))) v4f *)(p));
+#else
+  const v4f v = *(const __attribute__((address_space(1))) v4f *)(p);
+#endif
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+// (2-bit code tiles keep the default policy: nt measured 46.1 -> 45.0 sweeps/s at C2 2-bit, while
+// the f32 stream gained 29.8 -> 30.8; profiles/r03nt_ab.log)
+__device__ __forceinline__ uint4 ldg16_stream(const uint8_t *p) {
+  const v4u v = *(const __attribute__((address_space(1))) v4u *)(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 // column held (lanes with (lane & 3) == 0) after wave_reduce16
 __device__ __forceinline__ int reduce16_col(int lane) {
@@ -3047,14 +3068,14 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       const int64_t gb = d.gblk[s];  // wave-uniform
       const int64_t c0 = gb * B + w * CPW + c * CW;
 #pragma unroll
-      for (int j = 0; j < CW; ++j) x[j] = ldg4(d.X + min(c0 + j, d.M - 1) * ld + off);
-      const uint4 cg = *reinterpret_cast<const uint4 *>(d.xcodes + ((c0 >> 4) * d.ldc + (off >> 2)) * 16);
+      for (int j = 0; j < CW; ++j) x[j] = ldg4_stream(d.X + min(c0 + j, d.M - 1) * ld + off);
+      const uint4 cg = ldg16_stream(d.xcodes + ((c0 >> 4) * d.ldc + (off >> 2)) * 16);
       x[CW] = make_float4(__uint_as_float(cg.x), __uint_as_float(cg.y), __uint_as_float(cg.z), __uint_as_float(cg.w));
     } else if constexpr (XF) {
       static_assert(CW == 16, "a 2-bit item is one 16-column group");
       const int64_t gb = d.gblk[s];  // wave-uniform
       const int64_t grp = gb * (B >> 4) + ((w * CPW + c * CW) >> 4);
-      x[0] = *reinterpret_cast<const uint4 *>(d.Xc + (grp * d.ldc + (off >> 2)) * 16);
+      x[0] = ldg16_stream(d.Xc + (grp * d.ldc + (off >> 2)) * 16);
     } else {
       const float *base = d.X + off;
       // (scalar loads of the member indices instead: -6 % at C2, a K$ miss per item)
@@ -3062,10 +3083,10 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
 #pragma unroll
       for (int j = 0; j < CW; j += 4) {
         const int4 m = m4[j / 4];  // same LDS address in every lane: broadcast
-        x[j + 0] = ldg4(base + (int64_t)__builtin_amdgcn_readfirstlane(m.x) * ld);
-        x[j + 1] = ldg4(base + (int64_t)__builtin_amdgcn_readfirstlane(m.y) * ld);
-        x[j + 2] = ldg4(base + (int64_t)__builtin_amdgcn_readfirstlane(m.z) * ld);
-        x[j + 3] = ldg4(base + (int64_t)__builtin_amdgcn_readfirstlane(m.w) * ld);
+        x[j + 0] = ldg4_stream(base + (int64_t)__builtin_amdgcn_readfirstlane(m.x) * ld);
+        x[j + 1] = ldg4_stream(base + (int64_t)__builtin_amdgcn_readfirstlane(m.y) * ld);
+        x[j + 2] = ldg4_stream(base + (int64_t)__builtin_amdgcn_readfirstlane(m.z) * ld);
+        x[j + 3] = ldg4_stream(base + (int64_t)__builtin_amdgcn_readfirstlane(m.w) * ld);
       }
     }
   };
