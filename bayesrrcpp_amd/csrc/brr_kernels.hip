@@ -1743,10 +1743,11 @@ __device__ __forceinline__ void chain_hs_resident(int bs, const double *Lr0, con
 // is: ballot -> owner lane -> read delta -> update the later positions from the LDS Gram row.
 // A position found outside its window is re-decided at its current num (wave-uniform) and
 // re-examined; an exact-formula position is evaluated by decide_bayesr (BayesRv2.cpp:195-242).
-// coef is the block's Gram in LDS with the entries (i, j) for position i NOT before position j
-// zeroed (chain_coefficients with unit scale), so a step updates every position unconditionally
-// (earlier ones subtract 0) and the fast step has no divergent branch: branches cost the
-// persistent solver far more than their instructions (Horseshoe chain).
+// coef is the block's raw Gram in LDS (rows and columns by Gram index); a step updates the later
+// positions by a select on the position, so the fast step has no divergent branch: branches cost
+// the persistent solver far more than their instructions (Horseshoe chain).
+// (Until round 3 a coefficient pass zeroed the entries of earlier positions first: 128 KiB of LDS
+// rewritten per block at B = 128.)
 template <int B>
 __device__ __forceinline__ void chain_bayesr_resident(const Dev &d, int bs, double sigmaE, const double *Lr0,
                                                       const double *Llo, const double *Lhi, const double *Ldsel,
@@ -1859,10 +1860,13 @@ __device__ __forceinline__ void chain_bayesr_resident(const Dev &d, int bs, doub
       ++nslow;
       if (prof) tslow += wall_clock64() - ts0;
     }
-    // every position: the row's entries at positions <= first are 0 (and delta may be 0)
+    // the positions after `first` subtract G delta (a select, not a branch: the raw Gram block is
+    // in LDS, no coefficient pass zeroes the entries of earlier positions)
 #pragma unroll
     for (int q = 0; q < NS; ++q) {
-      r[q] = r[q] - grow[gg[q]] * delta;
+      const double g = grow[gg[q]];
+      const bool later = lane * NS + q > first && ((valid >> q) & 1u);
+      r[q] = later ? r[q] - g * delta : r[q];
       const double tt = r[q] * r[q];
       win = (win & ~(1u << q)) | ((uint32_t)(tt >= lo[q] && tt <= hi[q]) << q);
     }
@@ -2280,11 +2284,12 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     }
   }
   const uint64_t tA2 = prof ? wall_clock64() : 0;  // cross-Gram correction done
-  if (resident) {
-    // the chain's coefficients made in place from the resident Gram before the wait for the
-    // streaming side: entry (i, j) = G_ij / D_j (Horseshoe: D is a per-sweep constant,
-    // HorseshoeR.cpp:226-232) or G_ij (BayesR) when position i comes before position j, else 0;
-    // the scratch behind the rows holds the scale and the position of every Gram index
+  if (resident && HS) {
+    // the Horseshoe chain's coefficients made in place from the resident Gram before the wait for
+    // the streaming side: entry (i, j) = G_ij / D_j (D is a per-sweep constant,
+    // HorseshoeR.cpp:226-232) when position i comes before position j, else 0; the scratch behind
+    // the rows holds the scale and the position of every Gram index.  (The BayesR chain reads the
+    // raw Gram block and masks by position.)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces landed
     __syncthreads();  // (also: the correction's partial sums in the scratch are consumed)
     double *Linv = scr;
