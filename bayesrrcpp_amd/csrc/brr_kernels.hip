@@ -2113,7 +2113,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   const int gb = d.gblk[s];
   const int par = s % NPAR;
   const bool prof = d.sc->prof_on;
-  uint64_t tp0 = prof ? wall_clock64() : 0, tp1 = 0, tp2 = 0, tp3 = 0, tw = 0;
+  uint64_t tp0 = prof ? wall_clock64() : 0, tp1 = 0, tp2 = 0, tp3 = 0, tw = 0, tce = 0;
   const double sigmaE = d.sc->sigmaE;
   const int64_t S = d.nbB;
   const int64_t q0 = (int64_t)s * B;
@@ -2373,6 +2373,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   }
   const int nused = resident ? 0 : min(base, nst);  // resident: every row is in LDS already
   const int nov = max(base - nst, 0);  // predicted positions served by the ring
+  const int npred = base;
   if (t == 0) {
     *Lcons = 0;
     for (int k = 0; k < RS; ++k) Lready[k] = 0;
@@ -2507,6 +2508,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   } else if (!HS && t < 64) {
     chain_bayesr_rows<B>(d, bs, sigmaE, Lr0, Llo, Lhi, Ldsel, Lsdz, Lbo, Lbn, Lfl, Lks, Lgi, La, Lden, Lp, Lx2, Lz, Lm,
                          Lslot, Lspos, slots, d.gram + (int64_t)gb * B * B, RS, nst, nov, Lcons, Lready, prof);
+    if (prof) tce = wall_clock64();
   } else if (RS > 0 && nov > 0) {
     ring_produce<B, NW>(d.gram + (int64_t)gb * B * B, Lgi, Lspos, nst, nov, slots + (int64_t)nst * B, RS, Lcons,
                         Lready);
@@ -2616,6 +2618,9 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       atomicAdd(&d.sc->prof[14], (unsigned long long)(tA2 - tA1));
       atomicAdd(&d.sc->prof[15], (unsigned long long)(tA3 - tA2));
       atomicAdd(&d.sc->prof[11], (unsigned long long)(tc3 - tc2));
+      if (tce) atomicAdd(&d.sc->prof[17], (unsigned long long)(tp3 - tce));  // chain end -> all waves past it
+      atomicAdd(&d.sc->prof[18], (unsigned long long)nov);                     // rows served by the ring
+      atomicAdd(&d.sc->prof[19], (unsigned long long)npred);                   // positions predicted to change
     }
   }
 }

@@ -546,6 +546,10 @@ def main():
         diag["solve_chain_clock_ghz"] = round(s.scalar(121) / max(1.0, s.scalar(112)) * 0.1, 3)
         # serial chain loop alone (shader clocks per chain step; wave 0 of the solver)
         diag["solve_chain_loop_cycles_per_step"] = round(s.scalar(122) / max(1.0, s.scalar(116)), 1)
+        # (B >= 256 row chain) chain end -> every wave past the barrier, ring rows, predicted positions
+        diag["solve_after_chain_us"] = round(s.scalar(127) / calls / 100.0, 3)
+        diag["solve_ring_rows"] = round(s.scalar(128) / calls, 2)
+        diag["solve_predicted"] = round(s.scalar(129) / calls, 2)
         # streamer boundaries whose change list was prefetched (per streaming workgroup and block)
         nsg_ = int(s.scalar(104))
         if nsg_ > 0:
