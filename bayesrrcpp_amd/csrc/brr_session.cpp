@@ -1618,7 +1618,9 @@ int brr_session_sweep_local(brr_session *s) {
   if (!s) return -1;
   HIPCHK(hipSetDevice(s->device));
   int rc = do_sweep_local(s);
-  if (rc == 0) HIPCHK(hipStreamSynchronize(s->st));  // exchange buffers complete for the caller
+  // exchange buffers complete for the caller; a protocol timeout or failed residency census of
+  // this launch is reported here (as brr_session_sweep does), not left for a later sweep to trip on
+  if (rc == 0) rc = check_device_error(s);
   return rc;
 }
 

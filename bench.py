@@ -133,6 +133,9 @@ def parse():
     ap.add_argument("--cpu-sweeps", type=int, default=3)
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-roofline-events", action="store_true")
+    ap.add_argument("--exchanges", type=int, default=1,
+                    help="column shards: residual exchanges per sweep (1 = north_star's one all-reduce per sweep; "
+                         "more bound the stale-residual bias, DESIGN.md section 9)")
     ap.add_argument("--shard", default="cols", choices=["cols", "rows"],
                     help="N > 1: column shards with one residual all-reduce per sweep (north_star, SURVEY 8e; "
                          "default) or exact row shards with an all-reduce of each block's dots (SURVEY 8f4)")
@@ -395,7 +398,7 @@ def main():
         Pl, Nl = c1 - c0, N
         s = B.Session(model, N, Pl, K=K, groups=G, F=F, M_total=P, col_offset=c0, device=local_rank,
                       block_size=Bsz, order_mode=order_mode, shard_rank=rank, shard_count=world,
-                      x_storage=L.X_2BIT if x2 else L.X_F32)
+                      x_storage=L.X_2BIT if x2 else L.X_F32, exchanges_per_sweep=args.exchanges)
     # algorithmic bytes of one pass over this shard's genotypes (f32 values, or 2-bit codes + the
     # 16-B value table of every column)
     x_bytes = (Nl * Pl / 4.0 + 16.0 * Pl) if x2 else 4.0 * Nl * Pl
@@ -573,7 +576,7 @@ def main():
             "config": {"workload": cfg["workload"] + (" [2-bit genotype storage, SURVEY 8f3]" if x2 else ""),
                        "x_storage": args.x_storage, "N": N, "P": P, "K": K, "groups": G,
                        "block_size": Bsz, "order": args.order, "fused_stream_wg": int(s.scalar(104)), "code_cache": int(s.scalar(105)), "pipeline_lag": int(s.scalar(106)),
-                       "parallelism": f"row-shard x{world} (exact)" if rows else f"column-shard x{world}",
+                       "parallelism": f"row-shard x{world} (exact)" if rows else (f"column-shard x{world}" + (f", {args.exchanges} exchanges per sweep" if world > 1 else "")),
                        "setup_s": round(t_setup, 2), "diag": diag,
                        **({"output": emit} if emit else {})},
             "roofline": roof, "cpu_baseline": cpu,
