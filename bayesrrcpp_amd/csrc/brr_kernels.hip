@@ -1999,22 +1999,39 @@ __device__ __forceinline__ void chain_bayesr_rows(const Dev &d, int bs, double s
     if (delta != 0.0) {
       // the visited position's Gram row: its static slot, its ring entry, or HBM
       const int slf = __builtin_amdgcn_readlane(sll, L);
-      const double *grow = slf >= 0 ? slots + (int64_t)slf * B : Ggl + (int64_t)Lgi[first] * B;
+      int lrow = slf;  // LDS slot of the row, or -1: HBM
       bool from_ring = false;
       if (slf < 0 && RS > 0) {  // predicted beyond the static slots: its ring entry
         while (kc < nov && Lspos[nst + kc] < first) ++kc;  // entries passed without a change
         if (kc < nov && Lspos[nst + kc] == first && ring_take(Lcons, Lready, RS, kc)) {
-          grow = slots + (int64_t)(nst + kc % RS) * B;
+          lrow = nst + kc % RS;
           from_ring = true;
         }
       }
-      nglob += slf < 0 && !from_ring;
+      nglob += lrow < 0;
+      // the row's NS entries of this lane's positions, through a pointer of the row's own address
+      // space (a pointer that may be LDS or HBM compiles to FLAT loads, and the masked update
+      // below then became NS branches, each a FLAT load and a full vmcnt / lgkmcnt wait: ~3,300
+      // shader clocks per step at B = 512), all issued before any is used
+      double g[NS];
+      if (lrow >= 0) {
+        const __attribute__((address_space(3))) double *row =
+            (const __attribute__((address_space(3))) double *)(slots + (int64_t)lrow * B);
+#pragma unroll
+        for (int q = 0; q < NS; ++q) g[q] = row[gg[q]];
+      } else {
+        const __attribute__((address_space(1))) double *row =
+            (const __attribute__((address_space(1))) double *)(Ggl + (int64_t)Lgi[first] * B);
+#pragma unroll
+        for (int q = 0; q < NS; ++q) g[q] = row[gg[q]];
+      }
+#pragma unroll
+      for (int q = 0; q < NS; ++q) asm volatile("" ::"v"(g[q]));  // every load lands before the update
 #pragma unroll
       for (int q = 0; q < NS; ++q) {
         const int pos = lane * NS + q;
         const bool later = pos > first && pos < bs;
-        const double gq = grow[gg[q]];
-        r[q] = later ? r[q] - gq * delta : r[q];
+        r[q] = later ? r[q] - g[q] * delta : r[q];
         const double tt = r[q] * r[q];
         const uint32_t bw = (uint32_t)(tt >= lo[q] && tt <= hi[q]);
         win = later ? ((win & ~(1u << q)) | (bw << q)) : win;
