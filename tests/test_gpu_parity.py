@@ -165,6 +165,44 @@ def test_pipeline_modes_midsize(brr, oracle_mod, require_gpu, monkeypatch, mode)
         _compare(s, orc, O, L, L.MODEL_V2, tag=f"{mode} it={it}")
 
 
+def test_list_prefetch_engaged_and_bit_identical(brr, require_gpu, monkeypatch):
+    """The streamers' list prefetch (f32 storage: the change list of boundary s + 1 and its column rows
+    fetched into LDS while block s streams) serves boundaries in a streaming-bound sweep, and the chain
+    equals, bit for bit, that of a session with the prefetch switched off (BRR_LIST_PREFETCH=0: every
+    list applied by the ordinary path, itself pinned to the oracle by the parity tests above).  C2's
+    rows (100,000: two 256-row passes per streaming workgroup) on the on-device synthetic cohort with
+    32 causal markers, 128 blocks of 512 markers, lag 2 in every sweep.  (A sweep is streaming-bound
+    only when few markers change per block: a denser posterior keeps the solver the bound and its
+    lists are published too late to prefetch -- C2 itself: 93 % of the boundaries served.)"""
+    from bayesrrcpp_amd import _lib as L
+    monkeypatch.setenv("BRR_LAG", "2")
+    N, P = 100_000, 65_536
+
+    def make():
+        s = brr.Session(L.MODEL_V2, N, P, K=4, block_size=512)
+        s.synthesize(20261015, 0.5, 32)
+        s.set_bayesr(HYP["sigma0"], HYP["v0E"], HYP["s02E"], HYP["v0G"], HYP["s02G"], np.asarray(CVA, float), None)
+        s.init(3)
+        return s
+
+    s = make()
+    assert s.scalar(104) > 0  # the fused sweep
+    monkeypatch.setenv("BRR_LIST_PREFETCH", "0")
+    s0 = make()
+    for it in range(30):
+        if it == 20:  # past the burn-in (solver-bound: lists published too late to prefetch)
+            s.set_scalar(102, 1.0)  # diagnostics counters on (they count, nothing else changes)
+        s.sweep(1)
+        s0.sweep(1)
+        for w in (L.BETA, L.EPS, L.COMP):
+            assert np.array_equal(s.vector(w), s0.vector(w)), f"prefetch on/off differ ({w}) at sweep {it}"
+        assert s.scalar(L.SIGMAE) == s0.scalar(L.SIGMAE)
+    served = s.scalar(126)
+    s.close()
+    s0.close()
+    assert served > 0, "no boundary was served by the list prefetch"
+
+
 @pytest.mark.parametrize("B,xs", [(512, "f32"), (512, "2bit"), (256, "2bit")])
 def test_horseshoe_block512(brr, oracle_mod, require_gpu, B, xs):
     from bayesrrcpp_amd import _lib as L
