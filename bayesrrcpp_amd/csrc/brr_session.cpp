@@ -1090,14 +1090,16 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     if (rows || ref2bit || (pb && pb[0] == '1') || !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused, f32cc))
       s->fused = FusedCfg{};
     if (s->fused.nsg == 0) d.lag = 1;
-    // lag 1 while the solver bounds the sweep: more than ~9 changed markers per block at C2's
-    // 100,000 rows (measured crossover of the burn-in sweeps at B = 512, 37.4 against 38.7 ms per
-    // sweep over sweeps 5-24), scaled with the rows: a block's streaming time and a change's solver
-    // cost (one Gram-row and cross-Gram-row read each) both grow with B; BRR_LAG_SWITCH overrides the
-    // per-block count at 100,000 rows
+    // lag 1 while the solver bounds the sweep: more than ~15 changed markers per block at C2's
+    // 100,000 rows (measured crossover of the burn-in sweeps at B = 512; round 3, after the
+    // streamers' list prefetch and the row chain's typed loads: sweeps 5-24 at 34.01 / 34.14 ms
+    // against 34.14 / 34.27 at 9, 34.26 / 34.12 at 12, 34.23 / 34.12 at 20, 35.2 at 4,
+    // profiles/r03_lagswitch_ab.log), scaled with the rows: a block's streaming time and a change's
+    // solver cost (one Gram-row and cross-Gram-row read each) both grow with B; BRR_LAG_SWITCH
+    // overrides the per-block count at 100,000 rows
     {
       const char *ls = getenv("BRR_LAG_SWITCH");
-      const double per_block = (ls ? atof(ls) : 9.0) * ((double)N / 1e5);
+      const double per_block = (ls ? atof(ls) : 15.0) * ((double)N / 1e5);
       d.lag_thresh = lg ? 1e300 : per_block * s->nb;  // (BRR_LAG: that lag in every sweep)
     }
     // The streaming kernel's stream must never share a hardware queue with the session stream: a
