@@ -183,7 +183,10 @@ int brr_session_sweep(brr_session *s, int32_t n);
  * zeros before), finish sets eps = eps_segment_start + sum dEps and, after the last segment, draws
  * the hyper-parameters.  brr_session_exchanges_per_sweep() returns E.
  * Exchange buffers are device memory owned by the caller (e.g. torch tensors), sizes from
- * brr_session_exchange_sizes(). */
+ * brr_session_exchange_sizes().  sweep_local returns after the device work (the exchange buffers
+ * are complete) and, like brr_session_sweep, -3 with brr_last_error() when a device pipeline wait
+ * timed out or the fused sweep could not be made resident (later sweeps then use the per-block
+ * kernels). */
 int brr_session_exchange_sizes(brr_session *s, int64_t *n_eps, int64_t *n_stats);
 int brr_session_set_exchange(brr_session *s, double *dev_eps, double *dev_stats);
 /* session-owned exchange buffers (allocated on first use); host copies for gloo / tests:
