@@ -133,6 +133,11 @@ def test_r_stream_horseshoe_matches_device_chain(oracle_mod, data):
     dev = chain(seed=41, order_mode=O.ORDER_BLOCKED, block_size=64)
     ma, sa = _mean_se(r)
     mb, sb = _mean_se(dev)
-    cols = [0] + [2 + j for j in big]  # sigmaE and the large effects (tau: heavy-tailed)
+    cols = [0] + [2 + j for j in big]  # sigmaE and the large effects (tau compared on its log below)
     z = np.abs(ma - mb)[cols] / np.sqrt(sa ** 2 + sb ** 2)[cols]
     assert np.all(z < 4.0), (z, ma[cols], mb[cols])
+    # tau is heavy-tailed (its mean is dominated by rare excursions): the posterior mean of log tau
+    lta, lsa = _mean_se(np.log(r[:, 1:2]))
+    ltb, lsb = _mean_se(np.log(dev[:, 1:2]))
+    zt = float(np.abs(lta - ltb)[0] / np.sqrt(lsa ** 2 + lsb ** 2)[0])
+    assert zt < 4.0, (zt, lta, ltb)
