@@ -3917,8 +3917,13 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
   cap = std::max(cap, 1);
   // row ranges start on 256-B boundaries (64 rows): a range split inside a 128-B line costs
   // ~8 % of the streaming rate (measured); BRR_ROW_ALIGN overrides (diagnostics)
+  // B >= 256 (C2): whole 256-row passes per streaming workgroup, i.e. fewer and fuller workgroups
+  // (C2 f32: 196 x 512 rows instead of 224 x 448, 30.9 -> 31.8 sweeps/s, driver window 34.0 -> 33.3
+  // ms; 2-bit 46.5 -> 46.2, within noise, taken too so that both storages keep one geometry and
+  // bit-identical chains; profiles/r03_geometry_ab.log).  B = 128 (C3 / C4): unchanged within
+  // noise, kept at 64.
   const char *al = getenv("BRR_ROW_ALIGN");
-  const int64_t align = al && atoi(al) >= 4 ? (atoi(al) + 3) / 4 * 4 : 64;
+  const int64_t align = al && atoi(al) >= 4 ? (atoi(al) + 3) / 4 * 4 : (d.B >= 256 ? SROWS : 64);
   int64_t rpw = (d.N + cap - 1) / cap;
   rpw = std::max<int64_t>(SROWS, (rpw + align - 1) / align * align);
   const int nsg = (int)((d.N + rpw - 1) / rpw);

@@ -139,9 +139,9 @@ def test_v2_large_blocks(brr, oracle_mod, require_gpu, B, xs):
 @pytest.mark.parametrize("mode", ["persistent", "persistent-cap7", "persistent-cap30", "persistent-lag1", "per-block"])
 def test_pipeline_modes_midsize(brr, oracle_mod, require_gpu, monkeypatch, mode):
     """The sweep pipeline at a size with many streaming workgroups and reduction groups: the fused
-    persistent sweep (256 rows per streaming workgroup; 7 workgroups of 12 passes; 29 workgroups
-    of 704 rows -- row ranges start on 64-row boundaries -- the last one ragged; lag 2 and lag 1)
-    and the per-block kernels, all against the oracle over several sweeps."""
+    persistent sweep (256 rows per streaming workgroup; 7 workgroups of 12 passes; 27 workgroups
+    of 768 rows -- f32 row ranges at B >= 256 are whole 256-row passes -- the last one ragged; lag 2
+    and lag 1) and the per-block kernels, all against the oracle over several sweeps."""
     from bayesrrcpp_amd import _lib as L
     O = oracle_mod
     cap = {"persistent-cap7": 7, "persistent-cap30": 30}.get(mode)
@@ -155,7 +155,7 @@ def test_pipeline_modes_midsize(brr, oracle_mod, require_gpu, monkeypatch, mode)
     X, Y, _ = _cohort(O, N, 3000, n_causal=60)
     s, orc = _make(brr, O, L.MODEL_V2, X, Y, 0, B=512)
     if mode.startswith("persistent"):
-        rpw = max(256, (-(-N // cap) + 63) // 64 * 64) if cap else 256
+        rpw = max(256, (-(-N // cap) + 255) // 256 * 256) if cap else 256
         assert s.scalar(104) == -(-N // rpw)
     else:
         assert s.scalar(104) == 0
