@@ -160,7 +160,7 @@ def check(rc: int, what: str) -> int:
 
 def options(device=0, block_size=0, order_mode=ORDER_BLOCKED, shard_rank=0, shard_count=1,
             verbose=0, log=None, x_storage=X_F32, row_shard_rank=0, row_shard_count=1, row_offset=0,
-            N_total=0, exchanges_per_sweep=1) -> Options:
+            N_total=0, exchanges_per_sweep=0) -> Options:
     o = Options()
     lib().brr_options_default(C.byref(o))
     o.device, o.block_size, o.order_mode = device, block_size, order_mode

@@ -194,7 +194,9 @@ struct brr_session {
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
-  std::vector<std::pair<size_t, int>> ev_pairs;  // (start index, kind 0=stream 1=solve)
+  // (start event index, kind: 0 = k_stream, 1 = k_solve, 2 = solver per sweep, >= 3: a marker-loop
+  // launch over kind - 3 block positions -- the fused sweep, an exchange segment of it, the row-shard loop)
+  std::vector<std::pair<size_t, int>> ev_pairs;
   double t_stream = 0, t_solve = 0, t_solve_sweep = 0;
   int64_t n_stream = 0, n_solve = 0, n_solve_sweep = 0;
   std::vector<void *> allocs;
@@ -207,6 +209,9 @@ struct brr_session {
     return rc;
   }
   ~brr_session() {
+    // nothing may still run on either stream when its buffers go (e.g. a streaming kernel left in
+    // flight by a bounded solver timeout): both drain before any hipFree / hipEventDestroy
+    if (st_side) (void)hipStreamSynchronize(st_side);
     if (st) (void)hipStreamSynchronize(st);
     brr::sample_ring_close(this);
     if (comm) (void)ncclCommDestroy(comm);
@@ -216,7 +221,6 @@ struct brr_session {
     if (ev_go) (void)hipEventDestroy(ev_go);
     if (ev_done) (void)hipEventDestroy(ev_done);
     if (gram_codes) (void)hipFree(gram_codes);
-    if (st_side) (void)hipStreamSynchronize(st_side);
     if (st_side) (void)hipStreamDestroy(st_side);
     if (st) (void)hipStreamDestroy(st);
   }
@@ -248,7 +252,7 @@ int collect_timing(brr_session *s) {
     if (pr.second == 0) { s->t_stream += ms; s->n_stream++; }
     else if (pr.second == 1) { s->t_solve += ms; s->n_solve++; }
     else if (pr.second == 2) { s->t_solve_sweep += ms; s->n_solve_sweep++; }
-    else { s->t_stream += ms; s->n_stream += s->nb; }  // persistent streamer: per block position
+    else { s->t_stream += ms; s->n_stream += pr.second - 3; }  // marker-loop launch: per block position
   }
   s->ev_pairs.clear();
   s->ev_used = 0;
@@ -286,8 +290,10 @@ int upload_order(brr_session *s, const std::vector<int32_t> &order) {
   return 0;
 }
 
-// the pipeline's bounded device waits raise sc->err instead of hanging
-int check_device_error(brr_session *s) {
+// the pipeline's bounded device waits raise sc->err instead of hanging.  mid_sweep: called between
+// the exchange segments of a column-sharded sweep (brr_session_sweep_local), whose later segments
+// still run in the same sweep
+int check_device_error(brr_session *s, bool mid_sweep = false) {
   HIPCHK(hipStreamSynchronize(s->st));
   std::vector<int> sy(SY_WORDS);
   HIPCHK(hipMemcpy(sy.data(), s->d.sync, sizeof(int) * SY_WORDS, hipMemcpyDeviceToHost));
@@ -317,8 +323,18 @@ int check_device_error(brr_session *s) {
       const int NC = s->B >= 128 ? s->B / 128 : 1;
       HIPCHK(hipMemset(s->d.sync, 0, sizeof(int) * SY_WORDS));
       HIPCHK(hipMemset(s->d.cnt1, 0, sizeof(int) * NPAR * s->d.NG * NC));
-      s->sbase = s->abase = 0;
-      for (int k = 0; k < NPAR; ++k) s->gbase[k] = 0;
+      // The sweep's remaining segments (exchange segments, from block position f1 on) run on the
+      // per-block kernels with this sweep's epoch bases (Dev::sbase / gbase, set at segment 0):
+      // rebase them so that the counters, now zero, read as if blocks [0, f1) had passed, and the
+      // session's bases past this sweep.  Without a sweep in flight f1 = nb: the next sweep starts
+      // every epoch at zero.
+      int f1 = s->nb;
+      if (mid_sweep) f1 = (int)((int64_t)s->nb * (s->seg + 1) / s->nex);  // end of the failed segment
+      s->d.sbase = -f1;
+      for (int k = 0; k < NPAR; ++k) s->d.gbase[k] = -((f1 + NPAR - 1 - k) / NPAR);  // blocks < f1 of ring index k
+      s->sbase = s->d.sbase + s->nb;
+      for (int k = 0; k < NPAR; ++k) s->gbase[k] = s->d.gbase[k] + (s->nb + NPAR - 1 - k) / NPAR;
+      s->abase = 0;
       s->log("libbrr: fused sweep could not be made resident; using the per-block kernels\n");
     }
     return -3;
@@ -405,7 +421,7 @@ int do_sweep_local(brr_session *s) {
       HIPCHK(hipEventRecord(e0, s->st));
       HIPCHK(launch_sweep_fused(dp, it, s->fused, s->st, s->st_side, s->ev_go, s->ev_done));
       HIPCHK(hipEventRecord(e1, s->st));
-      s->ev_pairs.push_back({i0, 3});
+      s->ev_pairs.push_back({i0, 3 + (s1 - s0)});
     } else {
       HIPCHK(launch_sweep_fused(dp, it, s->fused, s->st, s->st_side, s->ev_go, s->ev_done));
     }
@@ -819,7 +835,7 @@ int coll_sweep_rows(Coll &c) {
   if (int rc = solve_b(nb - 1)) return rc;
   if (timed) {
     HIPCHK(hipEventRecord(s0->ev_pool[ti + 1], s0->st));
-    s0->ev_pairs.push_back({ti, 3});
+    s0->ev_pairs.push_back({ti, 3 + nb});
   }
   if (int rc = coll_each(c, [&](brr_session *s) -> int {
         Dev &d = s->d;
@@ -852,7 +868,7 @@ void brr_options_default(brr_options *o) {
   o->order_mode = BRR_ORDER_BLOCKED;
   o->shard_count = 1;
   o->row_shard_count = 1;
-  o->exchanges_per_sweep = 1;
+  o->exchanges_per_sweep = 0;  // automatic (column shards: the shard count)
 }
 
 const char *brr_last_error(void) { return g_last_error.c_str(); }
@@ -936,7 +952,18 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   s->K = K; s->G = groups; s->F = (int)F; s->B = B; s->model = model;
   s->order_mode = opt.order_mode;
   s->shard = opt.shard_rank; s->nshard = opt.shard_count;
-  s->nex = s->nshard > 1 ? std::max(1, opt.exchanges_per_sweep) : 1;
+  // column shards: exchanges per sweep E.  0 (default) = automatic: E = the shard count, at most the
+  // blocks per shard -- global quantities, so every shard runs the same E (the exchange is a
+  // collective).  One segment's stale residual of the other S - 1 shards is then (S - 1) / S^2 of a
+  // sweep's changes; 8 shards at E = 8 pass the distributional test against the 1-shard chain where
+  // E = 1 is biased by +2.9 % in sigmaE.
+  if (s->nshard > 1) {
+    const int64_t nbt = (M_total + B - 1) / B;
+    s->nex = opt.exchanges_per_sweep > 0 ? opt.exchanges_per_sweep
+                                         : (int)std::max<int64_t>(1, std::min<int64_t>(s->nshard, nbt / s->nshard));
+  } else {
+    s->nex = 1;
+  }
   s->rshard = rows ? opt.row_shard_rank : 0; s->nrshard = opt.row_shard_count;
   if (hipEventCreateWithFlags(&s->ev_x, hipEventDisableTiming) != hipSuccess) {
     set_error("cannot create an event on HIP device %d", s->device);
@@ -1510,20 +1537,35 @@ int brr_session_sweep(brr_session *s, int32_t n) {
       if (int rc = coll_sweep_rows(c)) return rc;
     return check_device_error(s);
   }
-  if (s->nshard > 1 && !s->comm) {
+  // BRR_EXCHANGE_LOOPBACK=1 (measurement): a column shard without a communicator sweeps as one rank of
+  // a multi-GPU job whose other ranks changed nothing -- the exchange buffers already hold the sum
+  // then -- so one GPU times a rank's real workload with every exchange segment, minus the collective
+  // itself (bench.py --rank-of)
+  static const bool loopback = getenv("BRR_EXCHANGE_LOOPBACK") && getenv("BRR_EXCHANGE_LOOPBACK")[0] == '1';
+  if (s->nshard > 1 && !s->comm && !loopback) {
     set_error("sharded session without a communicator: brr_session_comm_init, or drive "
               "sweep_local / exchange / sweep_finish yourself");
     return -1;
   }
   HIPCHK(hipSetDevice(s->device));
+  if (s->nshard > 1 && !s->comm)
+    if (int rc = brr_session_exchange_buffers(s, nullptr, nullptr)) return rc;
   for (int r = 0; r < n; ++r) {
     for (int e = 0; e < s->nex; ++e) {
+      const bool last = s->seg == s->nex - 1;
       if (int rc = do_sweep_local(s)) return rc;
-      if (s->nshard > 1) {
-        // the exchange step of the column-sharded sweep (E per sweep): sum of residual
-        // deltas (N doubles) and of the marker statistics, in place, on the session stream
-        ncclResult_t r1 = ncclAllReduce(s->ex_eps, s->ex_eps, (size_t)s->N, ncclDouble, ncclSum, s->comm, s->st);
-        ncclResult_t r2 = ncclAllReduce(s->ex_stats, s->ex_stats, (size_t)s->NS, ncclDouble, ncclSum, s->comm, s->st);
+      if (s->nshard > 1 && s->comm) {
+        // the exchange step of the column-sharded sweep (E per sweep): the sum of the
+        // residual deltas (N doubles) and, after the sweep's last segment only, of the marker
+        // statistics (NS; zeros before), in place on the session stream -- one collective when the
+        // two buffers are adjacent (the session's own, brr_session_exchange_buffers)
+        ncclResult_t r1 = ncclSuccess, r2 = ncclSuccess;
+        if (s->ex_stats == s->ex_eps + s->N) {
+          r1 = ncclAllReduce(s->ex_eps, s->ex_eps, (size_t)(s->N + (last ? s->NS : 0)), ncclDouble, ncclSum, s->comm, s->st);
+        } else {
+          r1 = ncclAllReduce(s->ex_eps, s->ex_eps, (size_t)s->N, ncclDouble, ncclSum, s->comm, s->st);
+          if (last) r2 = ncclAllReduce(s->ex_stats, s->ex_stats, (size_t)s->NS, ncclDouble, ncclSum, s->comm, s->st);
+        }
         if (r1 != ncclSuccess || r2 != ncclSuccess) {
           set_error("ncclAllReduce failed: %s", ncclGetErrorString(r1 != ncclSuccess ? r1 : r2));
           return -2;
@@ -1591,10 +1633,12 @@ int brr_session_set_exchange(brr_session *s, double *dev_eps, double *dev_stats)
 int brr_session_exchange_buffers(brr_session *s, double **dev_eps, double **dev_stats) {
   if (!s) return -1;
   if (!s->ex_eps || !s->ex_stats) {
+    // one allocation, the statistics right after the residual deltas: a sweep's exchange is then
+    // ONE ncclAllReduce of N + NS doubles (N alone after an earlier exchange segment)
     HIPCHK(hipSetDevice(s->device));
-    if (s->alloc(&s->ex_eps, s->N) || s->alloc(&s->ex_stats, s->NS)) return -2;
-    HIPCHK(hipMemset(s->ex_eps, 0, sizeof(double) * s->N));
-    HIPCHK(hipMemset(s->ex_stats, 0, sizeof(double) * s->NS));
+    if (s->alloc(&s->ex_eps, s->N + s->NS)) return -2;
+    s->ex_stats = s->ex_eps + s->N;
+    HIPCHK(hipMemset(s->ex_eps, 0, sizeof(double) * (s->N + s->NS)));
     s->ex_owned = true;
   }
   if (dev_eps) *dev_eps = s->ex_eps;
@@ -1622,7 +1666,7 @@ int brr_session_sweep_local(brr_session *s) {
   int rc = do_sweep_local(s);
   // exchange buffers complete for the caller; a protocol timeout or failed residency census of
   // this launch is reported here (as brr_session_sweep does), not left for a later sweep to trip on
-  if (rc == 0) rc = check_device_error(s);
+  if (rc == 0) rc = check_device_error(s, true);
   return rc;
 }
 
@@ -1656,6 +1700,7 @@ int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
     case 105: *out = (double)(s->fused.ccache || s->d.xcodes != nullptr); return 0;  // fused sweep: code cache in LDS
     case 106: *out = (double)s->d.lag; return 0;  // pipeline lag
     case 107: *out = (double)s->gram_np_init; return 0;  // Gram kernel: class planes of k_gram_int (0 = FP64 k_gram)
+    case 108: *out = (double)(s->fused.nsg > 0 && sc.lag_next >= 2 ? s->d.lag : 1); return 0;  // the next sweep's pipeline lag
     case 110: case 111: case 112: case 113: case 114: case 115: case 116: case 117: case 118: case 119:
     case 120: case 121: case 122: case 123: case 124: case 125: case 126: case 127: case 128: case 129:
       *out = (double)sc.prof[which - 110]; return 0;
@@ -1905,7 +1950,7 @@ brr_options options_from_caller(const brr_options *in) {
     else std::memcpy(&o, in, offsetof(brr_options, row_shard_rank));
     o.abi_version = BRR_ABI_VERSION;
   }
-  if (o.exchanges_per_sweep < 1) o.exchanges_per_sweep = 1;
+  if (o.exchanges_per_sweep < 0) o.exchanges_per_sweep = 0;
   return o;
 }
 

@@ -1,7 +1,7 @@
 """Column-sharded multi-GPU driver helpers: one process per GPU, markers split
 into contiguous ranges of whole blocks, the residual kept coherent by ONE all-reduce of the
-residual deltas (and the marker statistics) per sweep -- or per exchange segment, with
-brr_options.exchanges_per_sweep = E > 1 (E rounds per sweep).
+residual deltas (and the marker statistics) per exchange segment: brr_options.exchanges_per_sweep =
+E rounds per sweep (default: E = the shard count; 1 = one exchange per sweep).
 
 Two exchange paths share the same session protocol (brr_session_sweep_local -> sum ->
 brr_session_sweep_finish):
@@ -34,20 +34,36 @@ def init_native_comm(session, dist=None, rank: int = 0, world: int = 1):
 
 
 class HostExchange:
-    """Sweeps driven on the host: local sweep, gloo all-reduce of (deps, stats), finish."""
+    """Sweeps driven on the host: local sweep, gloo all-reduce of (deps, stats), finish.
+
+    A local sweep that fails on one rank (a device pipeline timeout or a failed residency census,
+    brr_session_sweep_local -> -3) must not leave its peers blocked in the collective: the failing
+    rank still takes part in the round's all-reduce, with a failure flag appended to the
+    statistics, and every rank finishes the round and then raises together."""
 
     def __init__(self, dist):
         self.dist = dist
 
     def sweep(self, shard, n: int = 1):
         """n sweeps; a sweep is `shard.exchanges_per_sweep` local / all-reduce / finish rounds."""
+        import numpy as np
         import torch
         rounds = getattr(shard, "exchanges_per_sweep", 1)
         for _ in range(n * rounds):
-            shard.sweep_local()
+            err = None
+            try:
+                shard.sweep_local()
+            except Exception as ex:  # noqa: BLE001 -- re-raised on every rank below
+                err = ex
             e, s = shard.exchange_get()
-            te, ts = torch.from_numpy(e), torch.from_numpy(s)
+            te = torch.from_numpy(e)
+            ts = torch.from_numpy(np.concatenate([s, [1.0 if err is not None else 0.0]]))
             self.dist.all_reduce(te)
             self.dist.all_reduce(ts)
-            shard.exchange_set(te.numpy(), ts.numpy())
+            failed = int(ts[-1].item())
+            shard.exchange_set(te.numpy(), ts[:-1].numpy())
             shard.sweep_finish()
+            if failed:
+                if err is not None:
+                    raise err
+                raise RuntimeError(f"column-shard sweep failed on {failed} other rank(s)")

@@ -29,7 +29,7 @@ class Session:
     def __init__(self, model, N, M, *, K=1, groups=1, F=0, M_total=None, col_offset=0,
                  device=0, block_size=0, order_mode=L.ORDER_BLOCKED, shard_rank=0,
                  shard_count=1, verbose=0, log=None, x_storage=L.X_F32, row_shard_rank=0,
-                 row_shard_count=1, row_offset=0, N_total=0, exchanges_per_sweep=1):
+                 row_shard_count=1, row_offset=0, N_total=0, exchanges_per_sweep=0):
         self._keep = []
         self.model, self.N, self.M, self.K, self.G, self.F = model, N, M, K, groups, F
         self.M_total = M if M_total is None else M_total

@@ -133,9 +133,14 @@ def parse():
     ap.add_argument("--cpu-sweeps", type=int, default=3)
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-roofline-events", action="store_true")
-    ap.add_argument("--exchanges", type=int, default=1,
-                    help="column shards: residual exchanges per sweep (1 = north_star's one all-reduce per sweep; "
-                         "more bound the stale-residual bias, DESIGN.md section 9)")
+    ap.add_argument("--exchanges", type=int, default=0,
+                    help="column shards: residual exchanges per sweep E (0 = the library's automatic E = the shard "
+                         "count, whose 8-shard chain matches the 1-shard chain; 1 = north_star's one all-reduce per "
+                         "sweep, biased from 2 shards on; DESIGN.md section 9)")
+    ap.add_argument("--rank-of", type=int, default=0, metavar="S",
+                    help="measurement: time ONE rank's real workload of an S-GPU column-sharded job on this GPU "
+                         "(shard 0 of S, every exchange segment, BRR_EXCHANGE_LOOPBACK=1: the other ranks' deltas "
+                         "taken as zero, so no collective); not a whole-job number")
     ap.add_argument("--shard", default="cols", choices=["cols", "rows"],
                     help="N > 1: column shards with one residual all-reduce per sweep (north_star, SURVEY 8e; "
                          "default) or exact row shards with an all-reduce of each block's dots (SURVEY 8f4)")
@@ -362,6 +367,9 @@ def main():
             sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to time a mislabelled run")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    emu = args.rank_of if world == 1 and args.rank_of > 1 else 0  # one rank of an emu-GPU job, emulated
+    if emu:
+        os.environ["BRR_EXCHANGE_LOOPBACK"] = "1"
     dist = None
     if world > 1:
         import torch.distributed as dist  # gloo only: rendezvous / barrier / max-over-ranks
@@ -391,14 +399,16 @@ def main():
                       order_mode=order_mode, row_shard_rank=rank, row_shard_count=world, row_offset=r0,
                       N_total=N, x_storage=L.X_2BIT if x2 else L.X_F32)
     else:
-        # contiguous block shards
+        # contiguous block shards (--rank-of S: shard 0 of S on this one GPU)
+        nshard, srank = (emu, 0) if emu else (world, rank)
         nb = (P + Bsz - 1) // Bsz
-        b0, b1 = nb * rank // world, nb * (rank + 1) // world
+        b0, b1 = nb * srank // nshard, nb * (srank + 1) // nshard
         c0, c1 = b0 * Bsz, min(P, b1 * Bsz)
         Pl, Nl = c1 - c0, N
         s = B.Session(model, N, Pl, K=K, groups=G, F=F, M_total=P, col_offset=c0, device=local_rank,
-                      block_size=Bsz, order_mode=order_mode, shard_rank=rank, shard_count=world,
+                      block_size=Bsz, order_mode=order_mode, shard_rank=srank, shard_count=nshard,
                       x_storage=L.X_2BIT if x2 else L.X_F32, exchanges_per_sweep=args.exchanges)
+    n_ex = s.exchanges_per_sweep
     # algorithmic bytes of one pass over this shard's genotypes (f32 values, or 2-bit codes + the
     # 16-B value table of every column)
     x_bytes = (Nl * Pl / 4.0 + 16.0 * Pl) if x2 else 4.0 * Nl * Pl
@@ -413,6 +423,8 @@ def main():
         g = torch.from_numpy(s.synth_partial_y())
         dist.all_reduce(g)
         s.synth_y(g.numpy(), args.data_seed, 0.5)
+    elif emu:  # Y from this shard's genetic values (the other shards' parts taken as zero)
+        s.synth_y(s.synth_partial_y(), args.data_seed, 0.5)
     if model == L.MODEL_HORSESHOE:
         s.set_horseshoe(A=(1 / N ** 0.5) * 1500 / (P - 1500), v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0,
                         c2=1.0, vC=10.0, sC=10.0)  # HorseshoeR.cpp:315-323
@@ -564,7 +576,7 @@ def main():
             diag["block_events_us"] = block_events(s.vector(201), int(s.scalar(106)))
         s.set_scalar(102, 0.0)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not emu and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, P)
     if rank == 0:
         out = {
@@ -576,7 +588,10 @@ def main():
             "config": {"workload": cfg["workload"] + (" [2-bit genotype storage, SURVEY 8f3]" if x2 else ""),
                        "x_storage": args.x_storage, "N": N, "P": P, "K": K, "groups": G,
                        "block_size": Bsz, "order": args.order, "fused_stream_wg": int(s.scalar(104)), "code_cache": int(s.scalar(105)), "pipeline_lag": int(s.scalar(106)),
-                       "parallelism": f"row-shard x{world} (exact)" if rows else (f"column-shard x{world}" + (f", {args.exchanges} exchanges per sweep" if world > 1 else "")),
+                       "parallelism": (f"row-shard x{world} (exact)" if rows
+                                       else f"column-shard rank 0 of {emu} emulated on 1 GPU, {n_ex} exchanges per sweep "
+                                            f"(other ranks' deltas zero, no collective; a per-rank rate, not a whole-job one)"
+                                       if emu else f"column-shard x{world}" + (f", {n_ex} exchanges per sweep" if world > 1 else "")),
                        "setup_s": round(t_setup, 2), "diag": diag,
                        **({"output": emit} if emit else {})},
             "roofline": roof, "cpu_baseline": cpu,

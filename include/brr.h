@@ -24,7 +24,7 @@
  *
  * The session API underneath (brr_session_*) is what the one-shot calls, tests and the
  * benchmark use: device-resident data, explicit sweeps, state read-back and the
- * column-sharded multi-GPU protocol (one process per GPU, residual exchange once per sweep).
+ * column-sharded multi-GPU protocol (one process per GPU, E residual exchanges per sweep).
  */
 #ifndef BRR_H
 #define BRR_H
@@ -81,11 +81,14 @@ typedef struct brr_options {
   int32_t row_shard_count; /* default 1 (no row sharding) */
   int64_t row_offset;      /* first global row of this shard */
   int64_t N_total;         /* rows of the whole cohort (0 = N) */
-  /* column shards (ABI 3): residual exchanges per sweep E (default 1 = once per sweep, SURVEY
-   * 8e).  Each shard's block positions split into E segments of whole blocks (segment e = blocks
-   * [nb e / E, nb (e + 1) / E)); after every segment the residual deltas are summed across the
-   * shards, so a shard sees the other shards' changes at most one segment late instead of one
-   * sweep (smaller stale-residual bias).  Ignored without column shards. */
+  /* column shards (ABI 3): residual exchanges per sweep E.  Each shard's block positions split into
+   * E segments of whole blocks (segment e = blocks [nb e / E, nb (e + 1) / E)); after every segment
+   * the residual deltas are summed across the shards, so a shard sees the other shards' changes at
+   * most one segment late instead of one sweep (stale-residual bias).
+   * 0 (default) = automatic: E = shard_count, capped at ceil(M_total / B) / shard_count -- the
+   * setting whose 8-shard chain matches the 1-shard chain within Monte-Carlo error.  1 = north_star's
+   * single exchange per sweep (measurably biased from 2 shards on).  Every shard must use the same E.
+   * Ignored without column shards. */
   int32_t exchanges_per_sweep;
 } brr_options;
 
@@ -185,11 +188,14 @@ int brr_session_sweep(brr_session *s, int32_t n);
  * Exchange buffers are device memory owned by the caller (e.g. torch tensors), sizes from
  * brr_session_exchange_sizes().  sweep_local returns after the device work (the exchange buffers
  * are complete) and, like brr_session_sweep, -3 with brr_last_error() when a device pipeline wait
- * timed out or the fused sweep could not be made resident (later sweeps then use the per-block
- * kernels). */
+ * timed out or the fused sweep could not be made resident (the sweep's later segments and sweeps
+ * then use the per-block kernels; a caller of the protocol still takes part in that round's exchange
+ * and may go on, or abort every rank together).  With a failed census the failed segment's markers
+ * keep their values this sweep (the state stays consistent). */
 int brr_session_exchange_sizes(brr_session *s, int64_t *n_eps, int64_t *n_stats);
 int brr_session_set_exchange(brr_session *s, double *dev_eps, double *dev_stats);
-/* session-owned exchange buffers (allocated on first use); host copies for gloo / tests:
+/* session-owned exchange buffers (allocated on first use; the statistics directly follow the N
+ * residual deltas, so brr_session_sweep's exchange is one all-reduce); host copies for gloo / tests:
  * dir 0 = device -> host, 1 = host -> device */
 int brr_session_exchange_buffers(brr_session *s, double **dev_eps, double **dev_stats);
 int brr_session_exchange_copy(brr_session *s, int32_t dir, double *host_eps, double *host_stats);
@@ -206,8 +212,9 @@ int brr_session_init_finish(brr_session *s);
 
 /* native multi-GPU: RCCL over xGMI, one process per GPU.  Rank 0 creates the 128-byte id,
  * the caller broadcasts it (MPI, a file, torch.distributed/gloo ...), every rank calls
- * brr_session_comm_init; brr_session_sweep then runs local sweep -> ncclAllReduce(sum) of
- * the exchange buffers on the session stream -> finish, with no host round trip.
+ * brr_session_comm_init; brr_session_sweep then runs, E times per sweep, local segment ->
+ * ncclAllReduce(sum) of the exchange buffers on the session stream (N + NS doubles after the last
+ * segment, N before) -> finish, with no host round trip.
  * Row-sharded sessions (row_shard_count > 1) take nranks = row_shard_count, rank =
  * row_shard_rank and must call it BEFORE brr_session_init (the Gram blocks are summed there);
  * their sweeps then all-reduce B partial dots per marker block (exact chain). */

@@ -15,7 +15,6 @@ def main():
     rank, world, port, out_dir, model = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], int(sys.argv[5])
     order = int(sys.argv[6]) if len(sys.argv) > 6 else 0
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-    import torch
     import torch.distributed as dist
     import bayesrrcpp_amd as brr
     from bayesrrcpp_amd import _lib as L
@@ -37,14 +36,12 @@ def main():
         s.set_bayesr(**HYP, cva=CVA)
     s.init(9)
     s.exchange_buffers()
-    for _ in range(4):
-        s.sweep_local()
-        e, st = s.exchange_get()
-        te, ts = torch.from_numpy(e), torch.from_numpy(st)
-        dist.all_reduce(te)
-        dist.all_reduce(ts)
-        s.exchange_set(te.numpy(), ts.numpy())
-        s.sweep_finish()
+    # the library's default exchanges per sweep (automatic: E = shard count), driven by the host
+    # protocol driver (local segment, gloo all-reduce of deltas + statistics + failure flag, finish)
+    from bayesrrcpp_amd.distributed import HostExchange
+    HostExchange(dist).sweep(s, 4)
+    assert s.iteration == 4
+    np.save(os.path.join(out_dir, f"E{rank}.npy"), np.array([s.exchanges_per_sweep]))
     np.save(os.path.join(out_dir, f"beta{rank}.npy"), s.vector(L.BETA))
     np.save(os.path.join(out_dir, f"eps{rank}.npy"), s.vector(L.EPS))
     comp = s.vector(L.COMP) if model != L.MODEL_HORSESHOE else np.zeros(c1 - c0)

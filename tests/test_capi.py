@@ -91,7 +91,7 @@ def test_options_struct_layout(brr, tmp_path):
     o = _lib.options()
     assert o.abi_version == _lib.ABI_VERSION == 3
     assert o.row_shard_count == 1 and o.row_shard_rank == 0 and o.N_total == 0
-    assert o.exchanges_per_sweep == 1
+    assert o.exchanges_per_sweep == 0  # automatic (column shards: E = shard count)
     src = tmp_path / "lay.c"
     fields = [f[0] for f in _lib.Options._fields_]
     src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "brr.h"\nint main(void){'

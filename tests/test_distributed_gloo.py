@@ -77,3 +77,59 @@ def test_shard_columns_partition():
             assert c0 % B == 0
             cover += list(range(c0, c1))
         assert cover == list(range(P))
+
+
+class _FlakyShard:
+    """Minimal protocol object (the session / oracle interface HostExchange drives) whose local
+    sweep fails on one rank in one round."""
+
+    exchanges_per_sweep = 2
+
+    def __init__(self, rank, fail_round):
+        self.rank, self.fail_round, self.round, self.finished = rank, fail_round, 0, 0
+
+    def sweep_local(self):
+        self.round += 1
+        if self.round == self.fail_round:
+            raise RuntimeError(f"sweep_local failed (rc=-3) on rank {self.rank}")
+
+    def exchange_get(self):
+        return np.full(4, float(self.rank + 1)), np.zeros(3)
+
+    def exchange_set(self, e, s):
+        assert np.array_equal(e, np.full(4, 3.0)) and s.shape == (3,)
+
+    def sweep_finish(self):
+        self.finished += 1
+
+
+def _flaky_worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from bayesrrcpp_amd.distributed import HostExchange
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sh = _FlakyShard(rank, fail_round=3 if rank == 1 else -1)
+    msg = ""
+    try:
+        HostExchange(dist).sweep(sh, 4)
+    except RuntimeError as ex:
+        msg = str(ex)
+    np.save(os.path.join(out_dir, f"flaky{rank}.npy"), np.array([sh.round, sh.finished]))
+    with open(os.path.join(out_dir, f"flaky{rank}.txt"), "w") as f:
+        f.write(msg)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_host_exchange_failure_stops_every_rank(tmp_path):
+    """A local sweep that fails on one rank (brr_session_sweep_local -> -3) still takes part in its
+    round's all-reduce (failure flag appended to the statistics): every rank finishes that round and
+    raises together instead of leaving its peers blocked in the collective."""
+    import torch.multiprocessing as mp
+    mp.spawn(_flaky_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        assert np.array_equal(np.load(tmp_path / f"flaky{r}.npy"), [3, 3])  # round 3 exchanged + finished, none after
+    assert "rank 1" in (tmp_path / "flaky1.txt").read_text()
+    assert "other rank" in (tmp_path / "flaky0.txt").read_text()

@@ -55,17 +55,24 @@ def test_c5_rank_workload(brr, require_gpu):
     s.init(1)
     Y = s.vector(L.EPS).copy()  # eps after init = Y - 0 - X 0
     s.exchange_buffers()
+    E = s.exchanges_per_sweep
+    assert E == R  # automatic: one exchange per shard count
     for it in range(10):
-        eps0, mu0 = s.vector(L.EPS), s.scalar(L.MU)
-        s.sweep_local()
-        mu1 = s.scalar(L.MU)
-        eps_start = (eps0 + mu0) - mu1  # the sweep start's shift (src/BayesRv2.cpp:177-179)
-        dE, stats = s.exchange_get()
-        eps_loc = s.vector(L.EPS)
-        assert np.array_equal(dE, eps_loc - eps_start), f"exchange buffer != eps_local - eps_start at sweep {it}"
-        # the seven other ranks contribute zero deltas and zero statistics: the sum is this rank's
-        s.exchange_set(dE, stats)
-        s.sweep_finish()
+        for e in range(E):
+            eps0, mu0 = s.vector(L.EPS), s.scalar(L.MU)
+            s.sweep_local()
+            mu1 = s.scalar(L.MU)
+            # the sweep start's shift (src/BayesRv2.cpp:177-179); later segments start from eps as is
+            eps_start = (eps0 + mu0) - mu1 if e == 0 else eps0
+            dE, stats = s.exchange_get()
+            eps_loc = s.vector(L.EPS)
+            assert np.array_equal(dE, eps_loc - eps_start), f"exchange buffer != eps_local - eps_start at {it}.{e}"
+            if e < E - 1:
+                assert not np.any(stats), "statistics follow the last segment only"
+            # the seven other ranks contribute zero deltas and zero statistics: the sum is this rank's
+            s.exchange_set(dE, stats)
+            s.sweep_finish()
+        assert s.iteration == it + 1
     beta, eps, mu = s.vector(L.BETA), s.vector(L.EPS), s.scalar(L.MU)
     xb = s.linear_predictor()
     sigmaE = s.scalar(L.SIGMAE)

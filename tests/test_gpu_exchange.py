@@ -28,6 +28,9 @@ def _rel(a, b):
 @pytest.mark.parametrize("model,E,per_block,lag", [
     (0, 2, False, None), (0, 4, False, None), (0, 3, False, "1"), (0, 4, True, None),
     (1, 3, False, None), (3, 3, False, None), (3, 2, True, None),
+    # lag 2 with segments of one block (E = 6) and of one or two blocks (E = 4): the cross-Gram
+    # corrections and the streamers' list prefetch must stop at the segment start
+    (0, 6, False, "2"), (0, 4, False, "2"),
 ])
 def test_exchange_segments_match_oracle(brr, oracle_mod, require_gpu, monkeypatch, model, E, per_block, lag):
     from bayesrrcpp_amd import _lib as L
@@ -49,6 +52,8 @@ def test_exchange_segments_match_oracle(brr, oracle_mod, require_gpu, monkeypatc
         s = brr.Session(model, N, 768, K=1 if model == L.MODEL_HORSESHOE else 4, groups=G, F=F, M_total=P,
                         col_offset=c0, block_size=B, shard_rank=r, shard_count=2, exchanges_per_sweep=E)
         assert s.exchanges_per_sweep == E
+        if lag == "2":
+            assert s.scalar(106) == 2  # the fused sweep's pipeline lag
         s.upload_x(X[:, c0:c0 + 768])
         s.set_y(Y)
         if model == L.MODEL_HORSESHOE:

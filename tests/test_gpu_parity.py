@@ -355,7 +355,8 @@ def test_sharded_two_sessions_match_oracle(brr, oracle_mod, require_gpu, xs):
     sess = []
     for r, (c0, pl) in enumerate(shards):
         s = brr.Session(L.MODEL_V2, N, pl, K=4, M_total=P, col_offset=c0, block_size=B,
-                        shard_rank=r, shard_count=2, x_storage=L.X_2BIT if xs == "2bit" else L.X_F32)
+                        shard_rank=r, shard_count=2, x_storage=L.X_2BIT if xs == "2bit" else L.X_F32,
+                        exchanges_per_sweep=1)  # (E > 1: tests/test_gpu_exchange.py)
         s.upload_x(X[:, c0:c0 + pl])
         s.set_y(Y)
         s.set_bayesr(**HYP, cva=CVA)
@@ -402,7 +403,7 @@ def test_sharded_reference_order_matches_oracle(brr, oracle_mod, require_gpu, mo
     for r, (c0, pl) in enumerate([(0, 256), (256, 256)]):
         s = brr.Session(model, N, pl, K=1 if model == L.MODEL_HORSESHOE else 4, groups=G, F=F, M_total=P,
                         col_offset=c0, block_size=B, shard_rank=r, shard_count=2, order_mode=L.ORDER_REFERENCE,
-                        x_storage=L.X_2BIT if xs == "2bit" else L.X_F32)
+                        x_storage=L.X_2BIT if xs == "2bit" else L.X_F32, exchanges_per_sweep=1)
         s.upload_x(X[:, c0:c0 + pl])
         s.set_y(Y)
         if model == L.MODEL_HORSESHOE:
@@ -457,7 +458,7 @@ def test_restart_column_shards(brr, oracle_mod, require_gpu):
     sess = []
     for r, c0 in enumerate((0, 256)):
         s = brr.Session(L.MODEL_RESTART, N, 256, K=len(CVA) + 1, groups=G, M_total=P, col_offset=c0,
-                        block_size=B, shard_rank=r, shard_count=2)
+                        block_size=B, shard_rank=r, shard_count=2, exchanges_per_sweep=1)
         s.upload_x(X[:, c0:c0 + 256])
         s.set_bayesr(HYP["sigma0"], HYP["v0E"], HYP["s02E"], HYP["v0G"], HYP["s02G"], cva2, gA[c0:c0 + 256])
         s.set_restart(st["mu0"], st["beta0"][c0:c0 + 256], st["sigmaE0"], st["sigmaGG0"], st["eps0"],
@@ -718,6 +719,88 @@ def test_failed_census_exits_cleanly(brr, oracle_mod, require_gpu, monkeypatch):
     resid = Y - s.scalar(L.MU) - X.astype(np.float64) @ s.vector(L.BETA)
     assert _rel(s.vector(L.EPS), resid) < 1e-9
     assert not np.array_equal(s.vector(L.EPS), eps0)
+
+
+def test_failed_census_in_exchange_segment(brr, oracle_mod, require_gpu, monkeypatch):
+    """A failed residency census in the FIRST of E = 4 exchange segments of a column shard: that
+    segment's markers keep their values for the sweep, and the sweep's remaining segments -- on the
+    per-block kernels, whose hand-over epochs are rebased past the failed segment -- and every later
+    sweep complete without a protocol timeout; eps = Y - mu - X beta holds and the replicated residual
+    stays bit-identical on both shards."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P, B, E = 300, 1536, 128, 4
+    X, Y, _ = O.synth_cohort(20261015, N, P, h2=0.5, n_causal=40)
+    sess = []
+    for r, c0 in enumerate((0, 768)):
+        s = brr.Session(L.MODEL_V2, N, 768, K=4, M_total=P, col_offset=c0, block_size=B, shard_rank=r,
+                        shard_count=2, exchanges_per_sweep=E)
+        s.upload_x(X[:, c0:c0 + 768]).set_y(Y).set_bayesr(**HYP, cva=CVA).init(9)
+        s.exchange_buffers()
+        sess.append(s)
+    assert all(s.scalar(104) > 0 for s in sess)
+
+    def rounds(n, fail_first=False):
+        for k in range(n):
+            for i, s in enumerate(sess):
+                if fail_first and k == 0 and i == 0:
+                    monkeypatch.setenv("BRR_TEST_CENSUS_EXTRA", "100000")
+                    with pytest.raises(L.BrrError, match="site 5"):
+                        s.sweep_local()
+                    monkeypatch.delenv("BRR_TEST_CENSUS_EXTRA")
+                else:
+                    s.sweep_local()
+            parts = [s.exchange_get() for s in sess]
+            te, ts = parts[0][0] + parts[1][0], parts[0][1] + parts[1][1]
+            for s in sess:
+                s.exchange_set(te, ts)
+                s.sweep_finish()
+
+    rounds(2 * E)
+    rounds(E, fail_first=True)
+    assert sess[0].scalar(104) == 0 and sess[1].scalar(104) > 0  # shard 0 on the per-block kernels now
+    assert all(s.iteration == 3 for s in sess)
+    rounds(2 * E)  # raises on a hand-over timeout
+    assert all(s.iteration == 5 for s in sess)
+    beta = np.concatenate([s.vector(L.BETA) for s in sess])
+    mu = sess[0].scalar(L.MU)
+    resid = Y - mu - X.astype(np.float64) @ beta
+    assert _rel(sess[0].vector(L.EPS), resid) < 1e-9
+    assert np.array_equal(sess[0].vector(L.EPS), sess[1].vector(L.EPS))
+    for s in sess:
+        s.close()
+
+
+def test_adaptive_lag_switch_matches_oracle(brr, oracle_mod, require_gpu, monkeypatch):
+    """The fused sweep's per-sweep pipeline lag (k_hyper: lag 1 while more markers change than
+    Dev::lag_thresh, else lag 2) flips within a few sweeps when BRR_LAG_SWITCH puts the threshold
+    inside the chain's own per-sweep change counts; both lags occur and the chain equals the oracle
+    (identical components, 1e-9) in every sweep, across the flips."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P, B, T = 2000, 4096, 256, 10
+    X, Y, _ = _cohort(O, N, P, n_causal=40)
+    orc = O.Oracle(O.V2, X, Y, cva=CVA, seed=5, order_mode=0, block_size=B, **HYP)
+    nz = []
+    for _ in range(T):
+        b0 = orc.vector(O.V_BETA)
+        orc.sweep(1)
+        nz.append(int(np.count_nonzero(orc.vector(O.V_BETA) != b0)))
+    # a threshold inside the burn-in's change counts: lag 1 while above it, lag 2 below
+    thr = 0.5 * (max(nz[1:]) + min(nz[1:]))
+    nb = P // B
+    monkeypatch.setenv("BRR_LAG_SWITCH", repr(thr / (N / 1e5) / nb))
+    s, orc = _make(brr, O, L.MODEL_V2, X, Y, 0, B=B, seed=5)
+    assert s.scalar(104) > 0 and s.scalar(106) == 2
+    lags = []
+    for it in range(T):
+        lags.append(int(s.scalar(108)))
+        s.sweep(1)
+        orc.sweep(1)
+        assert np.array_equal(s.vector(L.COMP), orc.vector(O.V_COMP)), f"it={it} lags={lags}"
+        assert _rel(s.vector(L.BETA), orc.vector(O.V_BETA)) < RTOL
+        assert _rel(s.vector(L.EPS), orc.vector(O.V_EPS)) < RTOL
+    assert 1 in lags and 2 in lags, (lags, nz, thr)
 
 
 @pytest.mark.parametrize("depth", [1, 4])
