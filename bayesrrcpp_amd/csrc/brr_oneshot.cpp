@@ -189,6 +189,34 @@ void hyper_warnings(const Log &log, double sigma0, double v0E, double s02E, doub
   if (neg) log("error: the variance of the components should be positive");
 }
 
+// BRR_TIMELINE=1: a host-side timeline of a one-shot call through the log callback -- one line per
+// phase (milliseconds since the call began): open + header, session create, X upload, setters,
+// init (Gram blocks), the chain (per 100 iterations: time in sweeps, in sample pushes), the writer's
+// drain and the teardown.  Accounts for the end-to-end time of the drop-in path beside the session
+// rate (bench.py --oneshot).
+struct Timeline {
+  bool on = false;
+  Log log;
+  std::chrono::steady_clock::time_point t0, last;
+  explicit Timeline(const Log &l) : log(l) {
+    const char *e = getenv("BRR_TIMELINE");
+    on = e && e[0] == '1';
+    t0 = last = std::chrono::steady_clock::now();
+  }
+  static double ms(std::chrono::steady_clock::duration d) {
+    return std::chrono::duration<double, std::milli>(d).count();
+  }
+  void mark(const char *phase) {
+    if (!on) return;
+    const auto t = std::chrono::steady_clock::now();
+    char b[160];
+    snprintf(b, sizeof b, "timeline %-10s +%9.2f ms  at %9.2f ms\n", phase, ms(t - last), ms(t - t0));
+    log(b);
+    last = t;
+  }
+};
+thread_local Timeline *g_tl = nullptr;  // the current one-shot call's timeline (run_chain reports into it)
+
 struct Run {
   int model;
   const char *out;
@@ -217,6 +245,8 @@ int run_chain(brr_session *s, const Run &r, CsvWriter *w) {
   w->bind(s, r.model, r.N, r.M, r.G, r.F);
   const auto t1 = std::chrono::steady_clock::now();
   const int every = r.max_it / 10;  // (int)std::ceil(max_iterations/10): integer division
+  double t_sweep = 0, t_push = 0;
+  int n_push = 0;
   for (int it = 0; it < r.max_it; ++it) {
     if (r.verbose && it > 0 && every > 0 && it % every == 0) {
       r.log("iteration: " + std::to_string(it) + "\n");
@@ -230,11 +260,24 @@ int run_chain(brr_session *s, const Run &r, CsvWriter *w) {
         r.log(b);
       }
     }
+    const auto ta = std::chrono::steady_clock::now();
     if (int rc = brr_session_sweep(s, 1)) return rc;
+    const auto tb = std::chrono::steady_clock::now();
+    t_sweep += std::chrono::duration<double, std::milli>(tb - ta).count();
     if (it >= r.burn_in && it % r.thin == 0) {
       int slot = -1;
       if (int rc = brr::sample_ring_push(s, &slot)) return rc;
       w->sample(slot, it);
+      t_push += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count();
+      ++n_push;
+    }
+    if (g_tl && g_tl->on && ((it + 1) % 100 == 0 || it + 1 == r.max_it)) {
+      char b[200];
+      snprintf(b, sizeof b, "timeline chain it %d: sweeps %.2f ms, %d sample pushes %.2f ms\n", it + 1, t_sweep,
+               n_push, t_push);
+      g_tl->log(b);
+      t_sweep = t_push = 0;
+      n_push = 0;
     }
   }
   brr_session_synchronize(s);
@@ -244,6 +287,7 @@ int run_chain(brr_session *s, const Run &r, CsvWriter *w) {
 }
 
 brr_options opts_or_default(const brr_options *o) { return brr::options_from_caller(o); }
+
 
 }  // namespace
 
@@ -255,6 +299,8 @@ int brr_BayesRSamplerV2(const char *outputFile, int seed, int max_iterations, in
                         const double *cva, int32_t n_cva, const brr_options *opt_in) {
   brr_options opt = opts_or_default(opt_in);
   Log log{opt.log, opt.log_userdata};
+  Timeline tl(log);
+  g_tl = &tl;
   FILE *f = fopen(outputFile, "w");  // BayesRv2.cpp:69
   if (!f) { log(std::string("brr: cannot open ") + outputFile + "\n"); return -3; }
   CsvWriter w(f);
@@ -265,19 +311,28 @@ int brr_BayesRSamplerV2(const char *outputFile, int seed, int max_iterations, in
     return 1;
   }
   hyper_warnings(log, sigma0, v0E, s02E, v0G, s02G, cva, n_cva);
+  tl.mark("open");
   brr_session *s = brr_session_create(BRR_MODEL_V2, N, M, M, 0, n_cva + 1, 1, 0, &opt);
+  tl.mark("create");
   int rc = s ? 0 : -1;
   if (!rc) rc = brr_session_upload_x_f64(s, X, N);
+  tl.mark("upload");
   if (!rc) rc = brr_session_set_y(s, Y);
   if (!rc) rc = brr_session_set_bayesr(s, sigma0, v0E, s02E, v0G, s02G, cva, nullptr);
+  tl.mark("set");
   if (!rc) rc = brr_session_init(s, seed);
+  tl.mark("init");
   Run r{BRR_MODEL_V2, outputFile, max_iterations, burn_in, thinning, N, M, 1, 0, log, opt.verbose != 0};
   if (!rc) rc = run_chain(s, r, &w);
+  tl.mark("chain");
   w.close();
   fclose(f);
+  tl.mark("drain");
+  g_tl = nullptr;
   if (!rc && w.error()) rc = w.error();
   if (rc) return fail(s, log, rc);
   brr_session_destroy(s);
+  tl.mark("destroy");
   return 0;
 }
 

@@ -315,10 +315,15 @@ def main_oneshot(args):
     os.makedirs(os.path.dirname(out), exist_ok=True)
     B.BayesRSamplerV2(out, args.seed, 5, 1, 1, X[:, :512].copy(order="F"), Y, HYP["sigma0"], HYP["v0E"],
                       HYP["s02E"], HYP["v0G"], HYP["s02G"], CVA, log=lambda m: None)  # warm (module load)
+    # host-side timeline of the timed call (libbrr BRR_TIMELINE: one line per phase and per 100
+    # iterations, through the log callback)
+    os.environ["BRR_TIMELINE"] = "1"
+    tl = []
     t0 = time.perf_counter()
     B.BayesRSamplerV2(out, args.seed, MAXIT, BURN, THIN, X, Y, HYP["sigma0"], HYP["v0E"], HYP["s02E"],
-                      HYP["v0G"], HYP["s02G"], CVA, log=lambda m: None)
+                      HYP["v0G"], HYP["s02G"], CVA, log=lambda m: tl.append(m.rstrip()) if m.startswith("timeline") else None)
     dt = time.perf_counter() - t0
+    os.environ.pop("BRR_TIMELINE")
     rows = sum(1 for _ in open(out)) - 1
     cpu = None
     if not args.no_cpu_baseline:
@@ -341,7 +346,7 @@ def main_oneshot(args):
         "data": "synthetic host cohort (numpy Binomial(2,f), standardised, f32-representable), f64 arithmetic",
         "config": {"workload": "C1: brr_BayesRSamplerV2 one-shot N=2,000 x P=10,000, 1,000 iterations, burn-in 500, "
                                "thinning 10 (BASELINE configs[0], vignettes/BayesRR.Rmd:93-100)",
-                   "wall_s": round(dt, 3), "csv_rows": rows, "csv_bytes": os.path.getsize(out)},
+                   "wall_s": round(dt, 3), "csv_rows": rows, "csv_bytes": os.path.getsize(out), "timeline": tl},
         "roofline": None, "cpu_baseline": cpu}), flush=True)
 
 

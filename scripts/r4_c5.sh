@@ -23,4 +23,8 @@ if [ "${C2:-1}" = 1 ]; then
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_c2.log 2>&1 || { echo "c2 failed"; tail -20 gpurun_out/${TAG}_c2.log; exit 1; }
   echo "== C2"; tail -1 gpurun_out/${TAG}_c2.log | cut -c1-420
 fi
+if [ "${ONESHOT:-1}" = 1 ]; then
+  timeout -k 10 300 python -u bench.py --oneshot --no-cpu-baseline > gpurun_out/${TAG}_c1_oneshot.log 2>&1 || { echo "oneshot failed"; tail -20 gpurun_out/${TAG}_c1_oneshot.log; exit 1; }
+  echo "== C1 one-shot"; tail -1 gpurun_out/${TAG}_c1_oneshot.log | cut -c1-3000
+fi
 exit 0
