@@ -2715,10 +2715,14 @@ constexpr int FUSED_GROUP = FUSED_GROUP_N;
 #ifndef BRR_APPLY_SMALL
 #define BRR_APPLY_SMALL 16
 #endif
+// (The split is defined over APPLY_NW = 8 waves whatever the streaming workgroup's width: a wider
+// workgroup's extra waves take whole passes of one-part lists or sit a long list out, so a residual
+// row sees the same operations in the same order under every streamer geometry.)
+constexpr int APPLY_NW = 8;
 __device__ __forceinline__ int apply_nparts(int np, int npass) {
-  return (npass >= SWEEP_NW || np <= BRR_APPLY_SMALL) ? 1 : SWEEP_NW / npass;
+  return (npass >= APPLY_NW || np <= BRR_APPLY_SMALL) ? 1 : APPLY_NW / npass;
 }
-template <int XF>
+template <int XF, int NT = SWEEP_NT>
 __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0, int64_t r1, int npass,
                                               double *eps_l, int *s_pidx, double *s_pbo, double *s_pbn,
                                               int *s_np, double *s_part, const int *msrc = nullptr,
@@ -2791,7 +2795,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
   const int ldp = npass * SROWS;                          // doubles per part in s_part
   if (np > 0) {
     const int p0 = G == 1 ? w : w % npass, part = G == 1 ? 0 : w / npass;
-    const int pstep = G == 1 ? SWEEP_NW : npass;  // (G > 1: one pass per wave)
+    const int pstep = G == 1 ? NT / 64 : npass;  // (G > 1: one pass per wave)
     const int e0 = part < G ? (np * part / G) : np, e1 = part < G ? (np * (part + 1) / G) : np;
     // the part's real entries: the neutral padding's products are exact zeros and are skipped
     const int ee = min(e1, nr);
@@ -2903,13 +2907,13 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
     if (ptime) { ptime[0] += tq1 - tq0; ptime[1] += tq2 - tq1; }
     if (G > 1) {
       // parts without a pass (G npass < 8 waves, or an empty part) hold nothing: zero them first
-      for (int i = t; i < G * ldp; i += SWEEP_NT) {
+      for (int i = t; i < G * ldp; i += NT) {
         const int part = i / ldp;
         if (np * part / G == np * (part + 1) / G) s_part[i] = 0.0;
       }
       __syncthreads();
       if (ptime) ptime[2] += wall_clock64() - tq2;
-      for (int i = t; i < ldp; i += SWEEP_NT) {
+      for (int i = t; i < ldp; i += NT) {
         if (r0 + i < r1) {
           double acc = s_part[i];
           for (int part = 1; part < G; ++part) acc += s_part[part * ldp + i];
@@ -3019,7 +3023,7 @@ __device__ __forceinline__ void apply_staged(const Dev &d, int np, int nr, doubl
 // Dev::slab_storage).  The value tables of the block being consumed are staged in LDS in storage
 // order (s_lut, B entries) at each block boundary, after the previous block's last item and
 // before the barrier that precedes the first item of the block.
-template <int CW, int P, int XF>
+template <int CW, int P, int XF, int NT = SWEEP_NT>
 __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int npass, double *eps_l, int *s_pidx,
                                             double *s_pbo, double *s_pbn, int *s_np, double *s_lut, int *s_mem,
                                             double *s_part, uint8_t *s_codes, int pfe = 0, int *s_pf = nullptr,
@@ -3046,7 +3050,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     if constexpr (XF) {
       const int gb = d.gblk[s], bs = d.bsz[s];
       const float4 *src = reinterpret_cast<const float4 *>(lutsrc) + (int64_t)gb * B;
-      for (int i = t; i < B; i += SWEEP_NT) {
+      for (int i = t; i < B; i += NT) {
         const float4 l = i < bs ? src[i] : make_float4(0.f, 0.f, 0.f, 0.f);
         double *dl = lut_of(s) + 4 * i;
         dl[0] = l.x; dl[1] = l.y; dl[2] = l.z; dl[3] = l.w;
@@ -3055,16 +3059,17 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   };
   // this launch's block positions [sb0, sb1): the sweep, or one exchange segment of it
   const int sb0 = d.seg0, sb1 = d.seg1;
-  for (int i = t; i < npass * SROWS; i += SWEEP_NT) eps_l[i] = r0 + i < r1 ? d.eps[r0 + i] : 0.0;
+  for (int i = t; i < npass * SROWS; i += NT) eps_l[i] = r0 + i < r1 ? d.eps[r0 + i] : 0.0;
   stage_lut(sb0);
   if (sb0 + 1 < sb1) stage_lut(sb0 + 1);
   // f32 path: the member (column) indices of blocks s and s + 1 live in LDS (s_mem[(s & 1) B ..]),
   // so an item's loads need no scalar-cache miss first; block s + 1's are copied at boundary s
   if constexpr (!XF)
-    for (int i = t; i < min(2, sb1 - sb0) * B; i += SWEEP_NT)
+    for (int i = t; i < min(2, sb1 - sb0) * B; i += NT)
       s_mem[(((sb0 + i / B) & 1) * B) + i % B] = d.member[(int64_t)sb0 * B + i];
   __syncthreads();
-  const int CPW = B / SWEEP_NW;  // columns per wave
+  constexpr int NW = NT / 64;
+  const int CPW = B / NW;  // columns per wave
   const int NCH = CPW / CW;      // chunks per wave and block
   // 2-bit storage with room in LDS: the code tiles of this workgroup's rows of the last LAG + 2
   // blocks (buffer s % NCC; [group][row quad][16 columns]), so the change list of block s-1-LAG is
@@ -3184,7 +3189,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
         if (s + 1 < sb1) stage_lut(s + 1);  // (its buffer is not read before the barrier)
       } else if (s + 1 < sb1) {
         __syncthreads();  // every wave is done issuing block s-1's items (same member buffer)
-        for (int i = t; i < B; i += SWEEP_NT) s_mem[((s + 1) & 1) * B + i] = d.member[(int64_t)(s + 1) * B + i];
+        for (int i = t; i < B; i += NT) s_mem[((s + 1) & 1) * B + i] = d.member[(int64_t)(s + 1) * B + i];
       }
       __syncthreads();
     }
@@ -3200,7 +3205,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
         if (pfe > 0) {
           fast = true;
 #pragma unroll
-          for (int q = 0; q < SWEEP_NW; ++q) fast = fast && s_pf[q] == a;
+          for (int q = 0; q < NW; ++q) fast = fast && s_pf[q] == a;
         }
       }
       pf_st = 0;
@@ -3232,7 +3237,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
           t_mark = tn;
         }
       }
-      apply_pending<XF>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, s_part,
+      apply_pending<XF, NT>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, s_part,
                         (!XF && s + 1 < sb1) ? d.member + (int64_t)(s + 1) * B : nullptr, s_mem + ((s + 1) & 1) * B,
                         cache_of(a), s_mem,
                         (XF && s + 1 < sb1) ? reinterpret_cast<const float4 *>(lutsrc) + (int64_t)d.gblk[s + 1] * B : nullptr,
@@ -3377,9 +3382,9 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   // end of the launch: the last LAG + 1 blocks' changes, then the residual rows back to HBM
   if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + sb1, d.sync, 4);
   for (int a = max(sb0, sb1 - 1 - LAG); a < sb1; ++a)
-    apply_pending<XF>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, s_part, nullptr, nullptr, cache_of(a),
-                      s_mem, nullptr, nullptr, lut_of(a));
-  for (int i = t; i < npass * SROWS; i += SWEEP_NT)
+    apply_pending<XF, NT>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, s_part, nullptr, nullptr,
+                          cache_of(a), s_mem, nullptr, nullptr, lut_of(a));
+  for (int i = t; i < npass * SROWS; i += NT)
     if (r0 + i < r1) d.eps[r0 + i] = eps_l[i];
 }
 
@@ -3387,6 +3392,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
 // partials of a group's 16 streaming workgroups, in workgroup order) into slab2, then
 // one arrival on the solver's counter.  Kept off the streaming workgroups, which go straight on
 // to the next block.
+template <int NT = SWEEP_NT>
 __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nred, bool prof) {
   const int t = threadIdx.x;
   const int ng = (nsg + FUSED_GROUP - 1) / FUSED_GROUP;
@@ -3399,7 +3405,7 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
       const int gw0 = grp * FUSED_GROUP, gsz = min(FUSED_GROUP, nsg - gw0);
       if (t == 0) wait_geq(d.cnt1 + par * d.NG + grp, (use + 1) * gsz, d.sync, 6);
       __syncthreads();
-      for (int cl = t; cl < B; cl += SWEEP_NT) {
+      for (int cl = t; cl < B; cl += NT) {
         double v16[FUSED_GROUP];
 #pragma unroll
         for (int q = 0; q < FUSED_GROUP; ++q) v16[q] = q < gsz ? ld_sc1(slab1 + (int64_t)(gw0 + q) * B + cl) : 0.0;
@@ -3497,16 +3503,19 @@ __global__ __launch_bounds__(SOLVE_NT, 1) void k_sweep_solve(Dev d, uint32_t it,
   solver_role<HS, B, SOLVE_NT>(d, it, nslot, smem);
 }
 
-template <int XF>
-__global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep_stream(Dev d, int nsg, int rpw, int npass, int nred, int ccache,
-                                                               int pfe) {
+// NT = 1024 (2-bit storage, B >= 256): 16 waves per streaming workgroup at <= 128 VGPRs -- four
+// waves per SIMD instead of two to hide the decode-dot's LDS-read -> FMA latency; every column's
+// partial dot and every residual update are the same operations in the same order as at NT = 512.
+template <int XF, int NT = SWEEP_NT>
+__global__ __launch_bounds__(NT, 1) void k_sweep_stream(Dev d, int nsg, int rpw, int npass, int nred, int ccache,
+                                                         int pfe) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_np[2];
   __shared__ int s_ok;
-  __shared__ int s_pf[SWEEP_NW];
+  __shared__ int s_pf[NT / 64];
   if (!sweep_census(d, nsg + 1 + nred, &s_ok)) return;
   if ((int)blockIdx.x >= nsg) {
-    reduce_role(d, (int)blockIdx.x - nsg, nsg, nred, d.sc->prof_on);
+    reduce_role<NT>(d, (int)blockIdx.x - nsg, nsg, nred, d.sc->prof_on);
     return;
   }
   double *eps_l = reinterpret_cast<double *>(smem);
@@ -3518,9 +3527,9 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep_stream(Dev d, int nsg, in
   uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_part + SWEEP_NW * SROWS) : nullptr;
   // (f32 storage) the list prefetch's staging area: pfe entries x npass passes x 1 KiB
   float *s_stage = reinterpret_cast<float *>(s_part + SWEEP_NW * SROWS);
-  stream_role<STREAM_CW, XF == 1 ? STREAM_P2 : STREAM_P, XF>(d, (int)blockIdx.x, rpw, npass, eps_l, s_pidx, s_pbo, s_pbn,
-                                                       s_np, s_lut, s_mem, s_part, s_codes, XF ? 0 : pfe, s_pf,
-                                                       s_stage);
+  stream_role<STREAM_CW, XF == 1 ? STREAM_P2 : STREAM_P, XF, NT>(d, (int)blockIdx.x, rpw, npass, eps_l, s_pidx, s_pbo,
+                                                           s_pbn, s_np, s_lut, s_mem, s_part, s_codes, XF ? 0 : pfe,
+                                                           s_pf, s_stage);
 }
 
 // ------------------------------------------------------------------------------------
@@ -3896,9 +3905,11 @@ static const void *solve_kernel(int model, int B) {
   }
 }
 
-// 0: f32 storage, 1: 2-bit codes, 2: f32 storage with the class-code cache (Dev::xcodes)
-static const void *stream_kernel(int xf) {
-  return xf == 1 ? (const void *)k_sweep_stream<1> : xf == 2 ? (const void *)k_sweep_stream<2> : (const void *)k_sweep_stream<0>;
+// 0: f32 storage, 1: 2-bit codes, 2: f32 storage with the class-code cache (Dev::xcodes); nt: threads
+// per streaming workgroup (1024: 2-bit codes only)
+static const void *stream_kernel(int xf, int nt = SWEEP_NT) {
+  if (xf == 1) return nt == 1024 ? (const void *)k_sweep_stream<1, 1024> : (const void *)k_sweep_stream<1>;
+  return xf == 2 ? (const void *)k_sweep_stream<2> : (const void *)k_sweep_stream<0>;
 }
 static int stream_variant(const Dev &d, const FusedCfg &c) { return d.Xc ? 1 : (c.f32cc && d.xcodes) ? 2 : 0; }
 
@@ -3934,8 +3945,12 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
   // BRR_FUSED_SINGLE=1: every role in the one cooperative k_sweep launch (the round-2 form)
   const char *one = getenv("BRR_FUSED_SINGLE");
   const bool split = !(one && one[0] == '1');
+  // 2-bit storage at B >= 256: 1,024-thread streaming workgroups (four waves per SIMD; each wave
+  // still a whole number of 16-column chunks); BRR_STREAM_NT=512 keeps eight waves (diagnostics)
+  const char *snt_env = getenv("BRR_STREAM_NT");
+  const int stnt = (split && xf && d.B % (16 * STREAM_CW) == 0 && !(snt_env && atoi(snt_env) == 512)) ? 1024 : SWEEP_NT;
   const void *fn = split ? solve_kernel(d.model, d.B) : sweep_kernel(d.model, d.B, xf);
-  const void *fst = split ? stream_kernel(xf ? 1 : 0) : nullptr;
+  const void *fst = split ? stream_kernel(xf ? 1 : 0, stnt) : nullptr;
   if (!fn) return false;
   hipFuncAttributes attr, attr_st;
   if (hipFuncGetAttributes(&attr, fn) != hipSuccess) return false;
@@ -3983,8 +3998,9 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
   cfg->pfe = pfe;
   if (split) {
     per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fst, SWEEP_NT, cfg->st_lds) != hipSuccess || per_cu != 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fst, stnt, cfg->st_lds) != hipSuccess || per_cu != 1)
       return false;
+    cfg->stnt = stnt;
     if (1 + nsg + nred > cus) return false;
   }
   cfg->nsg = nsg;
@@ -4011,7 +4027,7 @@ hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipS
     // the streaming kernel on the side stream, released by the same event that precedes the
     // solver on the session stream; the session stream waits for it before the next launch
     const int xv = stream_variant(d, c);
-    const void *fs = solve_kernel(d.model, d.B), *ft = stream_kernel(xv);
+    const void *fs = solve_kernel(d.model, d.B), *ft = stream_kernel(xv, xv == 1 ? c.stnt : SWEEP_NT);
     if (xv == 2) cc = 1;  // (k_sweep_stream<2> always keeps the cache)
     if (!fs || !ft) return hipErrorInvalidValue;
     int total = nsg + 1 + nred;
@@ -4022,7 +4038,8 @@ hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipS
     int pfe = xv == 0 ? c.pfe : 0;
     void *targs[] = {&dd, &nsg, &rpw, &npass, &nred, &cc, &pfe};
     if (e == hipSuccess)
-      e = hipLaunchKernel(ft, dim3((unsigned)(nsg + nred)), dim3(SWEEP_NT), targs, (unsigned)c.st_lds, st_side);
+      e = hipLaunchKernel(ft, dim3((unsigned)(nsg + nred)), dim3(xv == 1 ? c.stnt : SWEEP_NT), targs, (unsigned)c.st_lds,
+                          st_side);
     if (e == hipSuccess) e = hipEventRecord(ev_done, st_side);
     if (e == hipSuccess) e = hipStreamWaitEvent(st, ev_done, 0);
     return e;

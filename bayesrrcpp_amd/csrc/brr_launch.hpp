@@ -41,6 +41,7 @@ struct FusedCfg {
   int f32cc = 0;   // f32 storage: room for the class-code cache (used when Dev::xcodes is set: k_sweep_stream<2>)
   int split = 0;   // solver and streaming workgroups as two kernels side by side (else one k_sweep)
   int pfe = 0;     // (split, f32 storage) list entries the streamers can prefetch before a boundary (0: off)
+  int stnt = 512;  // (split) threads per streaming / reducing workgroup (1024: 2-bit codes at B >= 256)
   size_t lds = 0;     // solver workgroup's dynamic LDS (one kernel: every workgroup's)
   size_t st_lds = 0;  // (split) streaming / reducing workgroups' dynamic LDS
 };

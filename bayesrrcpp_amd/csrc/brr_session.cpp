@@ -1700,6 +1700,7 @@ int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
     case 105: *out = (double)(s->fused.ccache || s->d.xcodes != nullptr); return 0;  // fused sweep: code cache in LDS
     case 106: *out = (double)s->d.lag; return 0;  // pipeline lag
     case 107: *out = (double)s->gram_np_init; return 0;  // Gram kernel: class planes of k_gram_int (0 = FP64 k_gram)
+    case 109: *out = (double)(s->fused.nsg > 0 ? s->fused.stnt : 0); return 0;  // threads per streaming workgroup
     case 108: *out = (double)(s->fused.nsg > 0 && sc.lag_next >= 2 ? s->d.lag : 1); return 0;  // the next sweep's pipeline lag
     case 110: case 111: case 112: case 113: case 114: case 115: case 116: case 117: case 118: case 119:
     case 120: case 121: case 122: case 123: case 124: case 125: case 126: case 127: case 128: case 129:

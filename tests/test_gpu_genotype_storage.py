@@ -62,7 +62,7 @@ def _identical(a, b, L, model, tag):
         assert np.array_equal(a.vector(L.PI), b.vector(L.PI)), tag
 
 
-@pytest.mark.parametrize("model,B", [(0, 64), (0, 128), (0, 512), (1, 128), (3, 128)])
+@pytest.mark.parametrize("model,B", [(0, 64), (0, 128), (0, 256), (0, 512), (1, 128), (3, 128)])
 def test_2bit_chain_identical_to_f32(brr, oracle_mod, require_gpu, model, B):
     """Per-block path (B = 64), resident-Gram fused path (128) and the fused B = 512 path."""
     from bayesrrcpp_amd import _lib as L
@@ -86,6 +86,33 @@ def test_2bit_chain_identical_to_f32(brr, oracle_mod, require_gpu, model, B):
     orc.sweep(4)
     assert _rel(b.vector(L.BETA), orc.vector(O.V_BETA)) < RTOL
     assert _rel(b.vector(L.EPS), orc.vector(O.V_EPS)) < RTOL
+
+
+@pytest.mark.parametrize("B,cap", [(512, 4), (256, 2), (512, None)])
+def test_2bit_wide_streamer_identical(brr, oracle_mod, require_gpu, monkeypatch, B, cap):
+    """The 2-bit streaming kernel of 1,024-thread workgroups (B >= 256, four waves per SIMD) against
+    the same kernel at 512 threads (BRR_STREAM_NT=512) and against the f32 chain: bit-identical over
+    the burn-in's long change lists (split into parts across waves) and the steady state's short ones,
+    with one and several 256-row passes per streaming workgroup."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    N, P = 2000, 1536
+    X, Y, _ = O.synth_cohort(20261015, N, P, h2=0.5, n_causal=60)
+    if cap:
+        monkeypatch.setenv("BRR_STREAM_WG", str(cap))
+    wide = _session(brr, L, 0, X, Y, B, L.X_2BIT)
+    assert wide.scalar(104) > 0 and wide.scalar(109) == 1024
+    monkeypatch.setenv("BRR_STREAM_NT", "512")
+    narrow = _session(brr, L, 0, X, Y, B, L.X_2BIT)
+    assert narrow.scalar(109) == 512
+    f32 = _session(brr, L, 0, X, Y, B, L.X_F32)
+    for it in range(5):
+        for s in (wide, narrow, f32):
+            s.sweep(1)
+        _identical(wide, narrow, L, 0, f"B={B} cap={cap} it={it} 1024 vs 512")
+        _identical(wide, f32, L, 0, f"B={B} cap={cap} it={it} 2-bit vs f32")
+    for s in (wide, narrow, f32):
+        s.close()
 
 
 def test_2bit_synthetic_cohort_identical(brr, require_gpu):
