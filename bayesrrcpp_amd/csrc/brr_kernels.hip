@@ -3444,8 +3444,7 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_np[2];
   __shared__ int s_ok;
-  // residency census: every workgroup must be running before any waits on another.  (The
-  // cooperative launch guarantees it; the census is the defence.)  A workgroup whose census
+  // residency census: every workgroup must be running before any waits on another.  A workgroup whose census
   // timed out -- or that arrives after another one's did -- leaves before touching any state,
   // so a failed census costs one sweep's marker loop, never the chain's consistency.
   if (threadIdx.x == 0) {
@@ -3942,7 +3941,7 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
   const int nred = ngr(nsg);
   if (nsg > d.RG + 1) return false;  // slab1 rows
   const bool xf = d.Xc != nullptr;
-  // BRR_FUSED_SINGLE=1: every role in the one cooperative k_sweep launch (the round-2 form)
+  // BRR_FUSED_SINGLE=1: every role in one k_sweep grid (the PMC passes' form, launch_sweep_fused)
   const char *one = getenv("BRR_FUSED_SINGLE");
   const bool split = !(one && one[0] == '1');
   // 2-bit storage at B >= 256: 1,024-thread streaming workgroups (four waves per SIMD; each wave
@@ -4015,8 +4014,11 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
   return true;
 }
 
-// A cooperative launch: the runtime starts the grid only when every workgroup can be resident
-// at once (or fails the launch), which the in-kernel hand-over relies on.  BRR_TEST_CENSUS_EXTRA
+// The marker loop's launch.  Default: the solver kernel and the streaming kernel side by side on two
+// queues.  BRR_FUSED_SINGLE=1: every role in one k_sweep grid (the form PMC counter passes count:
+// counter collection serialises dispatches, so two co-dependent kernels cannot both run under it).
+// Both are plain launches: the in-kernel residency census (every workgroup running before any waits
+// on another, else all leave before touching state) guards the hand-over.  BRR_TEST_CENSUS_EXTRA
 // (tests) raises the census target above the grid to exercise the failed-census exit.
 hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipStream_t st, hipStream_t st_side,
                               hipEvent_t ev_go, hipEvent_t ev_done) {
@@ -4047,14 +4049,7 @@ hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipS
   const void *fn = sweep_kernel(d.model, d.B, d.Xc != nullptr);
   if (!fn) return hipErrorInvalidValue;
   void *args[] = {&dd, &it, &nslot, &nsg, &rpw, &npass, &nred, &cc};
-  // BRR_PLAIN_LAUNCH=1: a plain launch of the same kernel (the census then guards residency alone).
-  // Used for rocprofv3 runs: with ROCm 7.2's rocprofv3 attached, a process that made a cooperative
-  // launch segfaults in its exit handlers (after the profile is written); without the tool it exits
-  // cleanly (scripts/gpu_exitcrash.sh).
-  static const bool plain = getenv("BRR_PLAIN_LAUNCH") && getenv("BRR_PLAIN_LAUNCH")[0] == '1';
-  if (plain) return hipLaunchKernel(fn, dim3((unsigned)(c.nsg + 1 + c.nred)), dim3(SWEEP_NT), args, (unsigned)c.lds, st);
-  return hipLaunchCooperativeKernel(fn, dim3((unsigned)(c.nsg + 1 + c.nred)), dim3(SWEEP_NT), args,
-                                    (unsigned)c.lds, st);
+  return hipLaunchKernel(fn, dim3((unsigned)(c.nsg + 1 + c.nred)), dim3(SWEEP_NT), args, (unsigned)c.lds, st);
 }
 
 hipError_t launch_prep(const Dev &d, uint32_t it, hipStream_t st) {

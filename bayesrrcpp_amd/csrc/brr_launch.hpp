@@ -47,7 +47,7 @@ struct FusedCfg {
 };
 bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc = false);
 // split: the solver kernel on st, the streaming kernel on st_side (ev_go / ev_done order them
-// against st); otherwise one cooperative k_sweep on st
+// against st); otherwise one k_sweep grid on st (BRR_FUSED_SINGLE=1: the PMC passes' form)
 hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipStream_t st, hipStream_t st_side,
                               hipEvent_t ev_go, hipEvent_t ev_done);
 hipError_t launch_solve(const Dev &d, int s, uint32_t it, hipStream_t st);

@@ -22,9 +22,6 @@
 #include <thread>
 #include <vector>
 
-#include <execinfo.h>
-#include <signal.h>
-#include <unistd.h>
 
 #include <rccl/rccl.h>
 
@@ -62,30 +59,6 @@ struct Logger {
       return -2;                                                                       \
     }                                                                                  \
   } while (0)
-
-// Diagnostics (BRR_SEGV_TRACE=1): a fatal signal prints the faulting thread's host backtrace to
-// stderr before the default action -- used to locate the process-exit fault under rocprofv3
-// after a cooperative launch.
-void segv_trace(int sig, siginfo_t *si, void *) {
-  char head[128];
-  const int n = snprintf(head, sizeof head, "brr: signal %d at address %p, backtrace:\n", sig, si ? si->si_addr : nullptr);
-  if (write(2, head, (size_t)n) < 0) {}
-  void *fr[64];
-  backtrace_symbols_fd(fr, backtrace(fr, 64), 2);
-  signal(sig, SIG_DFL);
-  raise(sig);
-}
-__attribute__((constructor)) void install_segv_trace() {
-  const char *e = getenv("BRR_SEGV_TRACE");
-  if (!e || e[0] != '1') return;
-  struct sigaction sa;
-  memset(&sa, 0, sizeof sa);
-  sa.sa_sigaction = segv_trace;
-  sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
-  sigaction(SIGSEGV, &sa, nullptr);
-  sigaction(SIGBUS, &sa, nullptr);
-  sigaction(SIGABRT, &sa, nullptr);
-}
 
 void set_error(const char *fmt, ...) {
   char buf[1024];

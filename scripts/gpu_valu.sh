@@ -5,7 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out
 cd "$GRAFT_REPO_ROOT"
 # (counter collection serialises dispatches: the one-kernel form of the sweep's roles, plain launch)
-export TMPDIR=/tmp BRR_PLAIN_LAUNCH=1 BRR_FUSED_SINGLE=1
+export TMPDIR=/tmp BRR_FUSED_SINGLE=1
 for xs in ${XS_LIST:-2bit f32}; do
   timeout -k 10 -s KILL 240 rocprofv3 --pmc VALUBusy SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT \
     --kernel-include-regex 'k_sweep' -d gpurun_out/${TAG:-valu}_$xs -o pmc --output-format csv \

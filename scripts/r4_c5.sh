@@ -23,6 +23,14 @@ if [ "${C2:-1}" = 1 ]; then
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_c2.log 2>&1 || { echo "c2 failed"; tail -20 gpurun_out/${TAG}_c2.log; exit 1; }
   echo "== C2"; tail -1 gpurun_out/${TAG}_c2.log | cut -c1-420
 fi
+for cfg in ${EXTRA:-c2_2bit:--config,c2,--x-storage,2bit c2_2bit_nt512:--config,c2,--x-storage,2bit,--env,BRR_STREAM_NT=512}; do
+  name=${cfg%%:*}; args=$(echo ${cfg#*:} | tr ',' ' ')
+  envs=""; bargs=""
+  set -- $args
+  while [ $# -gt 0 ]; do if [ "$1" = "--env" ]; then envs="$envs $2"; shift 2; else bargs="$bargs $1"; shift; fi; done
+  env $envs timeout -k 10 300 python -u bench.py --steps 20 --warmup 10 --no-cpu-baseline $bargs > gpurun_out/${TAG}_$name.log 2>&1 || { echo "$name failed"; tail -20 gpurun_out/${TAG}_$name.log; exit 1; }
+  echo "== $name"; tail -1 gpurun_out/${TAG}_$name.log | cut -c1-420
+done
 if [ "${ONESHOT:-1}" = 1 ]; then
   timeout -k 10 300 python -u bench.py --oneshot --no-cpu-baseline > gpurun_out/${TAG}_c1_oneshot.log 2>&1 || { echo "oneshot failed"; tail -20 gpurun_out/${TAG}_c1_oneshot.log; exit 1; }
   echo "== C1 one-shot"; tail -1 gpurun_out/${TAG}_c1_oneshot.log | cut -c1-3000
