@@ -23,7 +23,7 @@ if [ "${C2:-1}" = 1 ]; then
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/${TAG}_c2.log 2>&1 || { echo "c2 failed"; tail -20 gpurun_out/${TAG}_c2.log; exit 1; }
   echo "== C2"; tail -1 gpurun_out/${TAG}_c2.log | cut -c1-420
 fi
-for cfg in ${EXTRA:-c2_2bit:--config,c2,--x-storage,2bit c2_2bit_nt512:--config,c2,--x-storage,2bit,--env,BRR_STREAM_NT=512}; do
+for cfg in ${EXTRA:-c2_2bit:--config,c2,--x-storage,2bit c2_2bit_nt512:--config,c2,--x-storage,2bit,--env,BRR_STREAM_NT=512 c4_cc_prof:--config,c4,--profile-solve,--env,BRR_F32_CODE_CACHE=1 c4_prof:--config,c4,--profile-solve}; do
   name=${cfg%%:*}; args=$(echo ${cfg#*:} | tr ',' ' ')
   envs=""; bargs=""
   set -- $args
