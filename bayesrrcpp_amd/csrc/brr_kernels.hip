@@ -55,6 +55,11 @@ __device__ __forceinline__ double block_sum(double v, double *lds /* NT/64 */) {
   return s;
 }
 
+// Workgroup barrier that orders LDS only: no vmcnt wait (a __syncthreads' release fence makes every
+// wave first wait for ALL its outstanding global accesses, LDS-DMA copies included).  For barriers
+// whose only cross-wave data is in LDS, where some waves have a copy in flight they wait for later.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
   int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
@@ -2147,60 +2152,68 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   const int gi_t = (prefgi && s > d.seg0) ? gi_pref : (t % B < bs ? d.gidx[q0 + t % B] : 0);
   if (prefgi && s + 1 < d.seg1) gi_pref = d.gidx[(int64_t)(s + 1) * B + t % B];
 
-  // A) everything that does not depend on k_stream(s).  The per-position constants are loaded
-  // first (vmcnt retires loads in order, so loads issued behind the 128 KiB Gram copy would wait
-  // for all of it), then resident mode starts the LDS-DMA of block s's Gram block (the previous
-  // block's copy is no longer read: its chain and write-back are done) so it lands while the
-  // cross-Gram correction is formed.
-#pragma unroll
-  for (int c = 0; c < NPT; ++c) {
-    const int pos = t + NT * c;
-    if (pos < bs) {
-      const int64_t q = q0 + pos;
-      const int gi = NPT == 1 ? gi_t : d.gidx[q];
-      double av[MAXK], dv[MAXK];
-#pragma unroll
-      for (int k = 0; k < MAXK; ++k) {
-        av[k] = k < K ? d.mc[(MC_A + k) * S + q] : 0.0;
-        dv[k] = k < KD ? d.mc[(MC_A + K + k) * S + q] : 0.0;
+  // A) everything that does not depend on k_stream(s): the per-position constants, the cross-Gram
+  // correction for the changes of the blocks the streamed dots have not seen, and (resident mode) the
+  // LDS-DMA of block s's Gram block.  The constants go straight from HBM into their LDS arrays by
+  // LDS-DMA (no registers, no wait at the issue), so they are in flight together with the
+  // correction's loads: one HBM round trip under the streaming load instead of two.  Deferred-DMA mode
+  // (persistent resident BayesR solver): waves NW/2 .. NW-1 alone copy the Gram block and do not wait
+  // for it until the chain -- the barriers between here and the chain only order LDS (lds_barrier), so
+  // the copy lands during the correction, the wait for the streaming side and the decisions -- while
+  // waves 0 .. NW/2-1 load the constants and form the correction; otherwise every wave does both (the
+  // Horseshoe's coefficient pass needs the Gram block before the wait).
+  const bool defer_dma = pipelined && !HS;
+  const int dma_w0 = defer_dma ? NW / 2 : 0;  // first wave of the Gram copy
+  const int cw1 = defer_dma ? NW / 2 : NW;    // waves [0, cw1) load the constants
+  {
+    // LDS [Lbo, Lden + KD B): fields bo, bn (= bo), x2, p, z, a_k (K), den_k (KD), B doubles each, in
+    // 16-B pieces (64 per wave instruction: 1 KiB contiguous in LDS, per-lane HBM sources); then
+    // [Lgi, Lm + B): the Gram index and the member of every position
+    const int nfd = 5 + K + KD;
+    const int npd = nfd * B / 2, npi = 2 * B / 4;  // 16-B pieces
+    const int ninst = (npd + 63) / 64 + (npi + 63) / 64;
+    for (int w = wv; w < ninst; w += cw1) {
+      const int nid = (npd + 63) / 64;
+      const __attribute__((address_space(1))) void *src;
+      __attribute__((address_space(3))) void *dst;
+      if (w < nid) {
+        const int pc = min(w * 64 + lane, npd - 1), f = pc / (B / 2), e = (pc % (B / 2)) * 2;
+        const int mf = f < 2 ? MC_BO : f == 2 ? MC_XSQ : f == 3 ? MC_P : f == 4 ? MC_Z : MC_A + (f - 5);
+        src = (const __attribute__((address_space(1))) void *)(d.mc + (int64_t)mf * S + q0 + e);
+        dst = (__attribute__((address_space(3))) void *)(reinterpret_cast<char *>(Lbo) + (int64_t)w * 1024);
+      } else {
+        const int pc = min((w - nid) * 64 + lane, npi - 1), f = pc / (B / 4), e = (pc % (B / 4)) * 4;
+        src = (const __attribute__((address_space(1))) void *)((f == 0 ? d.gidx : d.member) + q0 + e);
+        dst = (__attribute__((address_space(3))) void *)(reinterpret_cast<char *>(Lgi) + (int64_t)(w - nid) * 1024);
       }
-      const double bo = d.mc[MC_BO * S + q];
-      Lbo[pos] = bo;
-      Lbn[pos] = bo;
-      Lx2[pos] = d.mc[MC_XSQ * S + q];
-      Lp[pos] = HS ? 0.0 : d.mc[MC_P * S + q];
-      Lz[pos] = d.mc[MC_Z * S + q];
-      Lm[pos] = d.member[q];
-      Lgi[pos] = gi;
-#pragma unroll
-      for (int k = 0; k < MAXK; ++k) {
-        if (k < K) La[k * B + pos] = av[k];
-        if (k < KD) Lden[k * B + pos] = dv[k];
-      }
+      if (lane < (w < nid ? npd - w * 64 : npi - (w - nid) * 64))
+        __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
     }
   }
-  if (resident && !(pipelined && s > d.seg0 && misc[12] == s)) {
-    // row gi at slots + gi B, 1 KiB per wave-instruction; retired by each wave's vmcnt(0) and the
-    // barrier after it (before the coefficients / decisions read it).  (The persistent solver
-    // starts this copy at the end of the previous block already, see step 3.)
+  if (resident && !(pipelined && s > d.seg0 && misc[12] == s) && wv >= dma_w0) {
+    // row gi at slots + gi B, 1 KiB per wave-instruction; retired by each copying wave's vmcnt(0) and
+    // the barrier after it (before the coefficients / the chain read it).  (The persistent solver can
+    // start this copy at the end of the previous block already, see step 3.)
     constexpr int NCHUNK = B * B * 8 / 1024;
     const char *src = reinterpret_cast<const char *>(d.gram + (int64_t)gb * B * B);
     char *dst = reinterpret_cast<char *>(slots);
-    for (int c = wv; c < NCHUNK; c += NW)
+    for (int c = wv - dma_w0; c < NCHUNK; c += NW - dma_w0)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + c * 1024 + lane * 16),
                                        (__attribute__((address_space(3))) void *)(dst + c * 1024), 16, 0, 0);
   }
-  const uint64_t tA1 = prof ? wall_clock64() : 0;  // constants loaded (this thread's)
+  const uint64_t tA1 = prof ? wall_clock64() : 0;  // constants and copy issued
   // sum_i (x_j . x_i) delta_i over the changes of the blocks the streamed dots have not seen:
   // block s-1 (cross-Gram of cycle neighbours), and with lag 2 also block s-2 (cross-Gram of
   // blocks two apart), added in that order -- blocks of this launch only (seg0 onwards: the
   // earlier ones' changes are in the residual the launch started from).  The persistent solver
   // keeps the lists in LDS (written by its own write-back); the per-block solve stages the one list
-  // of its lag-1 pipeline from global memory into the slot area, which is free until step 2.  Every
-  // list's cross-Gram loads are issued together (one round trip per 16 entries, not per list).
-  // With B < NT the NT / B thread groups take contiguous parts of each list and their partial sums
-  // are added in group order.
-  constexpr int PG = B < NT ? NT / B : 1;
+  // of its lag-1 pipeline from global memory into the slot area, which is free until step 2.  Each
+  // round has up to 48 loads in flight: a chunk (16 entries) of every list, or with one list three
+  // of its chunks; every list is summed in entry order.  With B < NT the thread groups (NT / B, or
+  // the copy-free waves' share in deferred-DMA mode) take contiguous parts of each list and their
+  // partial sums are added in group order.
+  constexpr int PG0 = B < NT ? NT / B : 1;
+  const int PG = defer_dma ? max(1, min(PG0, (dma_w0 * 64) / B)) : PG0;
   double *scr = resident ? slots + (int64_t)B * B : slots;
   double *Lpart = scr + (B + 16) + (B + 16) / 2 + 1;  // [PG][B] partial sums (PG > 1)
   const int nlist = lag;  // (<= d.lag: the persistent solver's lag of this sweep; per-block: 1)
@@ -2250,8 +2263,8 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     const int pos = (t % (B < NT ? B : NT)) + NT * c;
     const int grp = B < NT ? t / B : 0;
     double corr[LAG_MAX] = {0.0, 0.0, 0.0};
-    if (pos < bs) {
-      const int gi = NPT == 1 ? gi_t : Lgi[pos];
+    if (pos < bs && grp < PG) {
+      const int gi = NPT == 1 ? gi_t : d.gidx[q0 + pos];  // (Lgi is still in flight)
       int c0[LAG_MAX], c1[LAG_MAX];
 #pragma unroll
       for (int l = 0; l < LAG_MAX; ++l) {
@@ -2259,26 +2272,31 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
         c0[l] = grp * nch / PG;
         c1[l] = (grp + 1) * nch / PG;
       }
-      // per round: the next chunk (16 entries) of every list in flight, then added in list order
+      // one list: three of its chunks per round (slot groups 0, 1, 2), else a chunk of every list
+      const bool one = nlist == 1;
       for (int k = 0;; ++k) {
         bool more = false;
         double cv[LAG_MAX][16];
+        int chs[LAG_MAX];
 #pragma unroll
-        for (int l = 0; l < LAG_MAX; ++l) {
-          const int ch = c0[l] + k;
+        for (int u3 = 0; u3 < LAG_MAX; ++u3) {
+          const int l = one ? 0 : u3;
+          const int ch = one ? c0[0] + 3 * k + u3 : c0[l] + k;
+          chs[u3] = ch;
           if (ch < c1[l]) {
             more = true;
 #pragma unroll
-            for (int u = 0; u < 16; ++u) cv[l][u] = Cl[l][(int64_t)Lgl[l][16 * ch + u] * B + gi];
+            for (int u = 0; u < 16; ++u) cv[u3][u] = Cl[l][(int64_t)Lgl[l][16 * ch + u] * B + gi];
           }
         }
         if (!more) break;
 #pragma unroll
-        for (int l = 0; l < LAG_MAX; ++l) {
-          const int ch = c0[l] + k;
+        for (int u3 = 0; u3 < LAG_MAX; ++u3) {
+          const int l = one ? 0 : u3;
+          const int ch = chs[u3];
           if (ch < c1[l]) {
 #pragma unroll
-            for (int u = 0; u < 16; ++u) corr[l] += cv[l][u] * Ldl[l][16 * ch + u];
+            for (int u = 0; u < 16; ++u) corr[l] += cv[u3][u] * Ldl[l][16 * ch + u];
           }
         }
       }
@@ -2286,16 +2304,18 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     // the lists' sums added in list order (per thread group, then the groups in group order)
     const double tot = (corr[0] + corr[1]) + corr[2];
     if (PG == 1) {
-      if (pos < bs) Lr0[pos] = tot;
-    } else {
+      if (pos < bs && grp == 0) Lr0[pos] = tot;
+    } else if (grp < PG) {
       Lpart[grp * B + pos] = tot;
     }
   }
+  // the constant-loading waves' LDS-DMA has landed before any wave reads the constants (the
+  // deferred Gram copy's waves wait for theirs just before the chain)
+  if (wv < cw1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (PG > 1) {
-    __syncthreads();
+    if (defer_dma) lds_barrier(); else __syncthreads();
     if (t < bs) {
       double tot = Lpart[t];
-#pragma unroll
       for (int g = 1; g < PG; ++g) tot += Lpart[g * B + t];
       Lr0[t] = tot;
     }
@@ -2322,8 +2342,12 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   if (t == 0 && s == 0) stamp(d.sync, 3);
   if (t == 0) wait_geq(d.sync + SY_GDONE + 32 * par, (d.gbase[par] + s / NPAR + 1) * d.gtarget, d.sync, 3);
   if (t == 0 && s == 0) stamp(d.sync, 4);
-  if (resident) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces landed
-  __syncthreads();
+  if (defer_dma) {
+    lds_barrier();  // (the copying waves wait for their pieces just before the chain)
+  } else {
+    if (resident) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA pieces landed
+    __syncthreads();
+  }
   if (prof) tw = wall_clock64();
   const double *slab2 = d.slab2 + par * d.slab2_stride;
   // 1) num at the block start, decisions with their windows; Gram-row slots for the positions
@@ -2376,7 +2400,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     }
     const uint64_t bal = __ballot(likely);
     if (lane == 0) misc[wv] = __popcll(bal);
-    __syncthreads();
+    if (defer_dma) lds_barrier(); else __syncthreads();
     int pre = base;
     for (int w = 0; w < wv; ++w) pre += misc[w];
     if (pos < bs) {
@@ -2386,7 +2410,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       if (likely) Lspos[idx] = pos;
     }
     for (int w = 0; w < NW; ++w) base += misc[w];
-    __syncthreads();
+    if (defer_dma) lds_barrier(); else __syncthreads();
   }
   const int nused = resident ? 0 : min(base, nst);  // resident: every row is in LDS already
   const int nov = max(base - nst, 0);  // predicted positions served by the ring
@@ -2414,6 +2438,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
         if (e0 + u * NT + t < tot) S2[e0 + u * NT + t] = v[u];
     }
   }
+  if (defer_dma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the copying waves' Gram pieces landed
   __syncthreads();
   if (prof) tp2 = wall_clock64();
   const uint64_t tc2 = prof ? __builtin_amdgcn_s_memtime() : 0;  // shader clock (diagnostics)
