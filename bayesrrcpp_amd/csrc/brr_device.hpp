@@ -119,6 +119,8 @@ struct Dev {
   int *cls_cnt;        // [M][4] real rows in each class
   int gram_np;         // k_gram_int's explicit class planes (1..3); 0 = the f64 matrix-core k_gram
   uint8_t *gram_codes; // k_gram_int's input: [nb][B/16][ldc][16] class codes of the current layout (k_encode_layout)
+  const uint8_t *xcls;   // REFERENCE order: every column's class codes, column-major (ldc bytes per column;
+                        // k_xcls), the source of each sweep's layout encoding (k_encode_gather), else nullptr
   const uint8_t *xcodes; // f32 storage, BLOCKED order: the class codes in storage order (gram_codes of the
                         // init layout), the source of the streamers' code cache (k_sweep_stream<2>), else nullptr
   const double *Y, *fixed, *cva;

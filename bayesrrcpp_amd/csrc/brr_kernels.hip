@@ -604,6 +604,66 @@ __global__ __launch_bounds__(256) void k_encode_layout(Dev d, uint8_t *Xk) {
   }
 }
 
+// REFERENCE order: every column's class codes once, column-major (ldc bytes per column, the classes of
+// rows 4g .. 4g+3 in byte g, PLINK packing), so that each sweep's layout encoding is a gather of
+// contiguous bytes (k_encode_gather) instead of a pass over X (f32: 4 N P bytes) or over the 2-bit
+// tiles (16-B granules, one useful byte each).  Rows beyond N: class 0 (k_gram_int masks them).
+__global__ __launch_bounds__(256) void k_xcls(Dev d, uint8_t *xcls) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= d.ldc) return;
+  for (int64_t col = blockIdx.y; col < d.M; col += gridDim.y) {
+    const int info = d.cls_info[col];
+    uint32_t byte = 0;
+    if (4 * g < d.N) {
+      if (d.Xc) {
+        const uint32_t c = d.Xc[code_off(col, g, d.B, d.ldc)];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) byte |= (((uint32_t)info >> (8 + 2 * ((c >> (2 * k)) & 3u))) & 3u) << (2 * k);
+      } else {
+        const float4 x = *reinterpret_cast<const float4 *>(d.X + col * d.ld + 4 * g);
+        const int nc = info & 7;
+        const float *v = d.cls_val + 4 * col;
+        const float v1 = v[1], v2 = v[2], v3 = v[3];
+        auto cl = [&](float xv) -> uint32_t {
+          return (nc > 1 && xv == v1) ? 1u : (nc > 2 && xv == v2) ? 2u : (nc > 3 && xv == v3) ? 3u : 0u;
+        };
+        byte = cl(x.x) | cl(x.y) << 2 | cl(x.z) << 4 | cl(x.w) << 6;
+      }
+    }
+    xcls[col * d.ldc + g] = (uint8_t)byte;
+  }
+}
+
+// The layout's class codes gathered from the column-major codes (k_xcls): thread = (16-position group q
+// of block b, 4 consecutive row quads); per position one 4-byte load (a wave reads 256 contiguous bytes
+// of a column), then the 16 positions' bytes of each quad as one 16-B store.  Same bytes as
+// k_encode_layout.
+__global__ __launch_bounds__(256) void k_encode_gather(Dev d, const uint8_t *xcls, uint8_t *Xk) {
+  const int64_t g0 = 4 * ((int64_t)blockIdx.x * 256 + threadIdx.x);
+  const int ng = d.B / 16;
+  if (g0 >= d.ldc) return;
+  for (int64_t bq = blockIdx.y; bq < (int64_t)d.nb * ng; bq += gridDim.y) {
+    const int b = (int)(bq / ng), q = (int)(bq % ng);
+    const int bs = d.bsz[b];
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int pos = 16 * q + i;
+      w[i] = pos < bs ? *reinterpret_cast<const uint32_t *>(xcls + (int64_t)d.member[(int64_t)b * d.B + pos] * d.ldc + g0)
+                      : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        o[j] = ((w[4 * j] >> (8 * k)) & 0xFFu) | ((w[4 * j + 1] >> (8 * k)) & 0xFFu) << 8 |
+               ((w[4 * j + 2] >> (8 * k)) & 0xFFu) << 16 | ((w[4 * j + 3] >> (8 * k)) & 0xFFu) << 24;
+      *reinterpret_cast<uint4 *>(Xk + (bq * d.ldc + g0 + k) * 16) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
 // Exact integer Gram of class-coded columns on the i8 matrix cores.  For columns i, j with class
 // values u_a, w_b and n_ab = #rows where column i is in class a and column j in class b,
 //     G_ij = sum_ab n_ab u_a w_b
@@ -3799,7 +3859,17 @@ hipError_t launch_classes(const Dev &d, int *flags, hipStream_t st) {
 hipError_t launch_encode_layout(const Dev &d, hipStream_t st) {
   if (!d.gram_codes) return hipErrorInvalidValue;
   const unsigned gy = (unsigned)std::min<int64_t>((int64_t)d.nb * (d.B / 16), 65535);
-  hipLaunchKernelGGL(k_encode_layout, dim3(cdiv64(d.ldc, 256), gy), dim3(256), 0, st, d, d.gram_codes);
+  if (d.xcls && d.ldc % 4 == 0)
+    hipLaunchKernelGGL(k_encode_gather, dim3(cdiv64(d.ldc / 4, 256), gy), dim3(256), 0, st, d, d.xcls, d.gram_codes);
+  else
+    hipLaunchKernelGGL(k_encode_layout, dim3(cdiv64(d.ldc, 256), gy), dim3(256), 0, st, d, d.gram_codes);
+  return hipGetLastError();
+}
+
+hipError_t launch_xcls(const Dev &d, uint8_t *xcls, hipStream_t st) {
+  if (d.M <= 0) return hipSuccess;
+  const unsigned gy = (unsigned)std::min<int64_t>(d.M, 65535);
+  hipLaunchKernelGGL(k_xcls, dim3(cdiv64(d.ldc, 256), gy), dim3(256), 0, st, d, xcls);
   return hipGetLastError();
 }
 

@@ -20,6 +20,7 @@ hipError_t launch_codes_tile(const uint8_t *src, uint8_t *Xc, int64_t c0, int64_
                              hipStream_t st);
 hipError_t launch_classes(const Dev &d, int *flags, hipStream_t st);
 hipError_t launch_encode_layout(const Dev &d, hipStream_t st);  // class codes of the layout (Dev::gram_codes)
+hipError_t launch_xcls(const Dev &d, uint8_t *xcls, hipStream_t st);  // column-major class codes (REFERENCE order)
 // Gram blocks: k_gram_int (exact, i8 matrix cores) when Dev::gram_np > 0, else k_gram (FP64 MFMA)
 hipError_t launch_gram(const Dev &d, int shift, double *G, double *GT, hipStream_t st);
 hipError_t launch_xsq(const Dev &d, hipStream_t st);

@@ -154,6 +154,7 @@ struct brr_session {
   bool x2bit = false;  // genotype storage: 2-bit codes (opt.x_storage == BRR_X_2BIT)
   int *cls_flags = nullptr;  // k_classes: [0] a column is not class-coded, [1] max classes per column
   uint8_t *gram_codes = nullptr;  // k_gram_int's input: class codes of the current Gram layout
+  uint8_t *xcls = nullptr;        // REFERENCE order: column-major class codes (Dev::xcls)
   int gram_np_init = 0;           // the Gram kernel of the latest init (Dev::gram_np then)
   double mu0 = 0, sigmaE0 = 0;
   double *ex_eps = nullptr, *ex_stats = nullptr;  // exchange buffers (caller- or session-owned)
@@ -163,6 +164,10 @@ struct brr_session {
   // reference visit order state
   GlibcRand grand;
   std::vector<int32_t> ref_order, ref_forder;
+  int32_t *ref_pin[2] = {nullptr, nullptr};  // pinned member buffers of upload_order
+  hipEvent_t ref_ev[2] = {nullptr, nullptr};
+  int ref_k = 0;
+  bool ref_static = false;  // block sizes and in-block indices of the REFERENCE layout uploaded
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -194,6 +199,11 @@ struct brr_session {
     if (ev_go) (void)hipEventDestroy(ev_go);
     if (ev_done) (void)hipEventDestroy(ev_done);
     if (gram_codes) (void)hipFree(gram_codes);
+    if (xcls) (void)hipFree(xcls);
+    for (int k = 0; k < 2; ++k) {
+      if (ref_pin[k]) (void)hipHostFree(ref_pin[k]);
+      if (ref_ev[k]) (void)hipEventDestroy(ref_ev[k]);
+    }
     if (st_side) (void)hipStreamDestroy(st_side);
     if (st) (void)hipStreamDestroy(st);
   }
@@ -244,22 +254,42 @@ std::vector<int32_t> shard_visit(const brr_session *s) {
 }
 
 int upload_order(brr_session *s, const std::vector<int32_t> &order) {
-  // positions s*B+i of the reference order; Gram blocks follow the positions
-  std::vector<int32_t> mem((size_t)s->nb * s->B, 0), gi((size_t)s->nb * s->B, 0), bsz(s->nb), gb(s->nb);
+  // positions s*B+i of the reference order; Gram blocks follow the positions.  Only the members change
+  // from sweep to sweep: they go through two pinned buffers (the copy of the sweep before last has
+  // landed before its buffer is refilled), so the host never waits for the device here and the next
+  // sweep's shuffle overlaps the current sweep's kernels; the block sizes and in-block indices are
+  // uploaded once.
+  const size_t n = (size_t)s->nb * s->B;
+  if (!s->ref_static) {
+    std::vector<int32_t> gi(n, 0), bsz(s->nb), gb(s->nb);
+    for (int b = 0; b < s->nb; ++b) {
+      const int size = (int)std::min<int64_t>(s->B, s->M - (int64_t)b * s->B);
+      bsz[b] = size;
+      gb[b] = b;
+      for (int i = 0; i < size; ++i) gi[(size_t)b * s->B + i] = i;
+    }
+    HIPCHK(hipMemcpyAsync(s->d.gidx, gi.data(), gi.size() * 4, hipMemcpyHostToDevice, s->st));
+    HIPCHK(hipMemcpyAsync(s->d.bsz, bsz.data(), bsz.size() * 4, hipMemcpyHostToDevice, s->st));
+    HIPCHK(hipMemcpyAsync(s->d.gblk, gb.data(), gb.size() * 4, hipMemcpyHostToDevice, s->st));
+    HIPCHK(hipStreamSynchronize(s->st));  // host vectors go out of scope
+    s->ref_static = true;
+  }
+  const int k = s->ref_k;
+  s->ref_k ^= 1;
+  if (!s->ref_pin[k]) {
+    HIPCHK(hipHostMalloc((void **)&s->ref_pin[k], n * 4, hipHostMallocDefault));
+    HIPCHK(hipEventCreateWithFlags(&s->ref_ev[k], hipEventDisableTiming));
+  } else {
+    HIPCHK(hipEventSynchronize(s->ref_ev[k]));  // this buffer's previous copy has landed
+  }
+  int32_t *mem = s->ref_pin[k];
   for (int b = 0; b < s->nb; ++b) {
     const int size = (int)std::min<int64_t>(s->B, s->M - (int64_t)b * s->B);
-    bsz[b] = size;
-    gb[b] = b;
-    for (int i = 0; i < size; ++i) {
-      mem[(size_t)b * s->B + i] = order[(size_t)b * s->B + i];
-      gi[(size_t)b * s->B + i] = i;
-    }
+    std::memcpy(mem + (size_t)b * s->B, order.data() + (size_t)b * s->B, sizeof(int32_t) * (size_t)size);
+    std::fill(mem + (size_t)b * s->B + size, mem + (size_t)(b + 1) * s->B, 0);
   }
-  HIPCHK(hipMemcpyAsync(s->d.member, mem.data(), mem.size() * 4, hipMemcpyHostToDevice, s->st));
-  HIPCHK(hipMemcpyAsync(s->d.gidx, gi.data(), gi.size() * 4, hipMemcpyHostToDevice, s->st));
-  HIPCHK(hipMemcpyAsync(s->d.bsz, bsz.data(), bsz.size() * 4, hipMemcpyHostToDevice, s->st));
-  HIPCHK(hipMemcpyAsync(s->d.gblk, gb.data(), gb.size() * 4, hipMemcpyHostToDevice, s->st));
-  HIPCHK(hipStreamSynchronize(s->st));  // host vectors go out of scope
+  HIPCHK(hipMemcpyAsync(s->d.member, mem, n * 4, hipMemcpyHostToDevice, s->st));
+  HIPCHK(hipEventRecord(s->ref_ev[k], s->st));
   return 0;
 }
 
@@ -583,6 +613,17 @@ int prepare_classes(brr_session *s) {
   }
   d.gram_codes = d.gram_np > 0 ? s->gram_codes : nullptr;
   s->gram_np_init = d.gram_np;
+  // REFERENCE order re-encodes its layout every sweep: from column-major class codes made once here
+  // (N P / 4 bytes; without the memory, from X itself as before)
+  if (d.gram_np > 0 && s->order_mode == BRR_ORDER_REFERENCE && !s->xcls && !getenv("BRR_NO_XCLS")) {
+    if (hipMalloc(&s->xcls, (size_t)s->M * d.ldc) != hipSuccess) {
+      (void)hipGetLastError();
+      s->xcls = nullptr;
+    } else {
+      HIPCHK(launch_xcls(d, s->xcls, s->st));
+    }
+  }
+  d.xcls = s->xcls;
   return 0;
 }
 
