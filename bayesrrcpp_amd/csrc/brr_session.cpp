@@ -168,6 +168,7 @@ struct brr_session {
   hipEvent_t ref_ev[2] = {nullptr, nullptr};
   int ref_k = 0;
   bool ref_static = false;  // block sizes and in-block indices of the REFERENCE layout uploaded
+  int census_failures = 0;  // fused sweeps whose residency census failed (the session then runs per block)
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -338,6 +339,7 @@ int check_device_error(brr_session *s, bool mid_sweep = false) {
       s->sbase = s->d.sbase + s->nb;
       for (int k = 0; k < NPAR; ++k) s->gbase[k] = s->d.gbase[k] + (s->nb + NPAR - 1 - k) / NPAR;
       s->abase = 0;
+      s->census_failures++;
       s->log("libbrr: fused sweep could not be made resident; using the per-block kernels\n");
     }
     return -3;
@@ -1714,6 +1716,7 @@ int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
     case 105: *out = (double)(s->fused.ccache || s->d.xcodes != nullptr); return 0;  // fused sweep: code cache in LDS
     case 106: *out = (double)s->d.lag; return 0;  // pipeline lag
     case 107: *out = (double)s->gram_np_init; return 0;  // Gram kernel: class planes of k_gram_int (0 = FP64 k_gram)
+    case 130: *out = (double)s->census_failures; return 0;  // residency census failures so far
     case 109: *out = (double)(s->fused.nsg > 0 ? s->fused.stnt : 0); return 0;  // threads per streaming workgroup
     case 108: *out = (double)(s->fused.nsg > 0 && sc.lag_next >= 2 ? s->d.lag : 1); return 0;  // the next sweep's pipeline lag
     case 110: case 111: case 112: case 113: case 114: case 115: case 116: case 117: case 118: case 119:

@@ -488,6 +488,9 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms = dt / args.steps * 1e3
+    if s.scalar(130) > 0:  # the fused sweep fell back to the per-block kernels: say so, loudly
+        print(f"bench.py: WARNING: {int(s.scalar(130))} fused sweep(s) failed the residency census; the "
+              "session ran the per-block kernels afterwards (see config.census_failures)", file=sys.stderr)
     diag = {"slow_steps_per_sweep": s.scalar(100) / (args.warmup + args.steps),
             "changed_per_sweep": s.scalar(101) / (args.warmup + args.steps),
             "nonzero_frac": 1.0 - float(s.vector(L.VCOUNT)[0]) / P if model != L.MODEL_HORSESHOE else 1.0}
@@ -593,6 +596,7 @@ def main():
             "config": {"workload": cfg["workload"] + (" [2-bit genotype storage, SURVEY 8f3]" if x2 else ""),
                        "x_storage": args.x_storage, "N": N, "P": P, "K": K, "groups": G,
                        "block_size": Bsz, "order": args.order, "fused_stream_wg": int(s.scalar(104)), "code_cache": int(s.scalar(105)), "pipeline_lag": int(s.scalar(106)), "stream_wg_threads": int(s.scalar(109)),
+                       "census_failures": int(s.scalar(130)),
                        "parallelism": (f"row-shard x{world} (exact)" if rows
                                        else f"column-shard rank 0 of {emu} emulated on 1 GPU, {n_ex} exchanges per sweep "
                                             f"(other ranks' deltas zero, no collective; a per-rank rate, not a whole-job one)"

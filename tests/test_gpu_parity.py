@@ -715,6 +715,7 @@ def test_failed_census_exits_cleanly(brr, oracle_mod, require_gpu, monkeypatch):
     monkeypatch.delenv("BRR_TEST_CENSUS_EXTRA")
     assert np.array_equal(s.vector(L.BETA), beta0)  # the marker loop never ran
     assert s.scalar(104) == 0                       # per-block kernels from now on
+    assert s.scalar(130) == 1                       # and the session counts the failure (bench.py reports it)
     s.sweep(3)
     resid = Y - s.scalar(L.MU) - X.astype(np.float64) @ s.vector(L.BETA)
     assert _rel(s.vector(L.EPS), resid) < 1e-9
@@ -759,6 +760,7 @@ def test_failed_census_in_exchange_segment(brr, oracle_mod, require_gpu, monkeyp
     rounds(2 * E)
     rounds(E, fail_first=True)
     assert sess[0].scalar(104) == 0 and sess[1].scalar(104) > 0  # shard 0 on the per-block kernels now
+    assert sess[0].scalar(130) == 1 and sess[1].scalar(130) == 0
     assert all(s.iteration == 3 for s in sess)
     rounds(2 * E)  # raises on a hand-over timeout
     assert all(s.iteration == 5 for s in sess)
