@@ -2814,7 +2814,7 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
                                               int *mdst = nullptr, const uint8_t *ccode = nullptr,
                                               int *s_ppos = nullptr, const float4 *lsrc = nullptr,
                                               double *ldst = nullptr, const double *lutb = nullptr, int lcnt = 0,
-                                              uint64_t *ptime = nullptr) {
+                                              uint64_t *ptime = nullptr, double *s_w = nullptr) {
 #pragma clang fp contract(off)
   // diagnostics (ptime, thread 0): [0] += list staging incl. its barrier, [1] += this wave's
   // products, [2] += the wait for the other waves' parts, [3] += the staging stores and the last
@@ -2853,6 +2853,11 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
         if (XF) {
           s_ppos[lane] = gi0;
           s_cb[lane] = ccode ? (int64_t)(gi0 >> 4) * (npass * 64 * 16) + (gi0 & 15) : code_off(col0, 0, d.B, d.ldc);
+          // the entry's value x delta table: the residual update adds W[code] per row, the product the
+          // f32 path forms as x * (b_old - b_new) (the same rounded product, then the same add)
+          const double *lt = lutb + 4 * gi0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) s_w[4 * lane + k] = lt[k] * pd0;
         }
         s_pd[lane] = pd0;
       }
@@ -2863,12 +2868,16 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
       const int es = e < nr ? e : max(nr - 1, 0);
       const int col = ld_sc1_int(pidx + es);
       s_pidx[e] = col;
+      const double pde = ld_sc1(pbo + e) - ld_sc1(pbn + e);
       if (XF) {
         const int gi = ld_sc1_int(d.pend_gi + slot * d.pend_stride + es);  // in-block (storage) index
         s_ppos[e] = gi;
         s_cb[e] = ccode ? (int64_t)(gi >> 4) * (npass * 64 * 16) + (gi & 15) : code_off(col, 0, d.B, d.ldc);
+        const double *lt = lutb + 4 * gi;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s_w[4 * e + k] = lt[k] * pde;
       }
-      s_pd[e] = ld_sc1(pbo + e) - ld_sc1(pbn + e);
+      s_pd[e] = pde;
     }
     if (lane == 0) { s_np[0] = np; s_np[1] = nr; }
   }
@@ -2909,13 +2918,12 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
 #pragma unroll
             for (int q = 0; q < AB; ++q) {
               if (e + q < ee) {
-                const double *lt = lutb + 4 * s_ppos[e + q];
+                const double *w = s_w + 4 * (e + q);  // x delta by code: one LDS read and one add per row
                 const uint32_t b = r[q];
-                const double dd = s_pd[e + q];
-                a0 = __builtin_fma(lt[b & 3u], dd, a0);
-                a1 = __builtin_fma(lt[(b >> 2) & 3u], dd, a1);
-                a2 = __builtin_fma(lt[(b >> 4) & 3u], dd, a2);
-                a3 = __builtin_fma(lt[(b >> 6) & 3u], dd, a3);
+                a0 = a0 + w[b & 3u];
+                a1 = a1 + w[(b >> 2) & 3u];
+                a2 = a2 + w[(b >> 4) & 3u];
+                a3 = a3 + w[(b >> 6) & 3u];
               }
             }
           };
@@ -2945,11 +2953,11 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
 #pragma unroll
         for (int q = 0; q < AB; ++q) {
           if (e + q < ee) {
-            const double dd = s_pd[e + q];  // (fused multiply-add, as the 2-bit path)
-            a0 = __builtin_fma((double)x[q].x, dd, a0);
-            a1 = __builtin_fma((double)x[q].y, dd, a1);
-            a2 = __builtin_fma((double)x[q].z, dd, a2);
-            a3 = __builtin_fma((double)x[q].w, dd, a3);
+            const double dd = s_pd[e + q];  // (rounded product, then the add: the 2-bit path's W[code])
+            a0 = a0 + (double)x[q].x * dd;
+            a1 = a1 + (double)x[q].y * dd;
+            a2 = a2 + (double)x[q].z * dd;
+            a3 = a3 + (double)x[q].w * dd;
           }
         }
       };
@@ -3056,10 +3064,10 @@ __device__ __forceinline__ void apply_staged(const Dev &d, int np, int nr, doubl
       for (int e = ap.e0; e < ee; ++e) {
         const double dd = readlane_f64(lpd, e);
         const float4 x = *reinterpret_cast<const float4 *>(stage + ((int64_t)e * npass + ap.p0) * SROWS + 4 * lane);
-        a0 = __builtin_fma((double)x.x, dd, a0);
-        a1 = __builtin_fma((double)x.y, dd, a1);
-        a2 = __builtin_fma((double)x.z, dd, a2);
-        a3 = __builtin_fma((double)x.w, dd, a3);
+        a0 = a0 + (double)x.x * dd;
+        a1 = a1 + (double)x.y * dd;
+        a2 = a2 + (double)x.z * dd;
+        a3 = a3 + (double)x.w * dd;
       }
       if (G == 1) {
         if (r0 + off < r1) {
@@ -3112,7 +3120,7 @@ template <int CW, int P, int XF, int NT = SWEEP_NT>
 __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int npass, double *eps_l, int *s_pidx,
                                             double *s_pbo, double *s_pbn, int *s_np, double *s_lut, int *s_mem,
                                             double *s_part, uint8_t *s_codes, int pfe = 0, int *s_pf = nullptr,
-                                            float *s_stage = nullptr) {
+                                            float *s_stage = nullptr, double *s_w = nullptr) {
 #pragma clang fp contract(off)
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -3327,7 +3335,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
                         cache_of(a), s_mem,
                         (XF && s + 1 < sb1) ? reinterpret_cast<const float4 *>(lutsrc) + (int64_t)d.gblk[s + 1] * B : nullptr,
                         lut_of(s + 1), lut_of(a), (XF && s + 1 < sb1) ? d.bsz[s + 1] : 0,
-                        (prof && t == 0) ? acc_sub : nullptr);
+                        (prof && t == 0) ? acc_sub : nullptr, s_w);
       if (prof && t == 0) {
         tr_last(d, s, TR_APPLY_LAST);
         if (s == nb / 2) d.trace[(int64_t)nb * 16 + 1024 + g] = wall_clock64();  // per-workgroup probe
@@ -3468,7 +3476,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + sb1, d.sync, 4);
   for (int a = max(sb0, sb1 - 1 - LAG); a < sb1; ++a)
     apply_pending<XF, NT>(d, a % NSLOT, r0, r1, npass, eps_l, s_pidx, s_pbo, s_pbn, s_np, s_part, nullptr, nullptr,
-                          cache_of(a), s_mem, nullptr, nullptr, lut_of(a));
+                          cache_of(a), s_mem, nullptr, nullptr, lut_of(a), 0, nullptr, s_w);
   for (int i = t; i < npass * SROWS; i += NT)
     if (r0 + i < r1) d.eps[r0 + i] = eps_l[i];
 }
@@ -3554,9 +3562,12 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
     // (2-bit storage: s_mem holds the change positions instead); the apply's partial sums; then
     // the code cache
     double *s_part = reinterpret_cast<double *>(s_mem + 2 * d.B);
-    uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_part + SWEEP_NW * SROWS) : nullptr;
+    // (table storage) the apply's value x delta tables, then the code cache
+    double *s_w = XF ? s_part + SWEEP_NW * SROWS : nullptr;
+    uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_w + (int64_t)(d.B + 16) * 4) : nullptr;
     stream_role<STREAM_CW, XF == 1 ? STREAM_P2 : STREAM_P, XF>(d, (int)blockIdx.x - 1, rpw, npass, eps_l, s_pidx, s_pbo,
-                                                         s_pbn, s_np, s_lut, s_mem, s_part, s_codes);
+                                                         s_pbn, s_np, s_lut, s_mem, s_part, s_codes, 0, nullptr, nullptr,
+                                                         s_w);
   }
 }
 
@@ -3608,12 +3619,14 @@ __global__ __launch_bounds__(NT, 1) void k_sweep_stream(Dev d, int nsg, int rpw,
   int *s_pidx = reinterpret_cast<int *>(s_pbn + (d.B + 16));
   int *s_mem = s_pidx + (d.B + 16);
   double *s_part = reinterpret_cast<double *>(s_mem + 2 * d.B);
-  uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_part + SWEEP_NW * SROWS) : nullptr;
+  // (table storage: 2-bit codes, f32 code cache) the apply's value x delta tables, then the code cache
+  double *s_w = XF ? s_part + SWEEP_NW * SROWS : nullptr;
+  uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_w + (int64_t)(d.B + 16) * 4) : nullptr;
   // (f32 storage) the list prefetch's staging area: pfe entries x npass passes x 1 KiB
   float *s_stage = reinterpret_cast<float *>(s_part + SWEEP_NW * SROWS);
   stream_role<STREAM_CW, XF == 1 ? STREAM_P2 : STREAM_P, XF, NT>(d, (int)blockIdx.x, rpw, npass, eps_l, s_pidx, s_pbo,
                                                            s_pbn, s_np, s_lut, s_mem, s_part, s_codes, XF ? 0 : pfe,
-                                                           s_pf, s_stage);
+                                                           s_pf, s_stage, s_w);
 }
 
 // ------------------------------------------------------------------------------------
@@ -4060,7 +4073,7 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
   // new betas), the member indices of two blocks in LDS
   // (f32 storage with a class-code cache: the value tables and code tiles as for 2-bit storage)
   const bool tables = xf || (f32cc && split);
-  const size_t lut_bytes = (size_t)d.B * 32 * (d.lag + 3);
+  const size_t lut_bytes = (size_t)d.B * 32 * (d.lag + 3) + (size_t)(d.B + 16) * 32;  // + the apply's x delta tables
   const size_t eps_base = (size_t)npass * SROWS * sizeof(double) + (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int)) +
                           2 * sizeof(int) * d.B + (size_t)SWEEP_NW * SROWS * sizeof(double);
   const size_t code_bytes = (size_t)(d.lag + 2) * d.B * npass * 64;
