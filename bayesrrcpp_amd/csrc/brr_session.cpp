@@ -968,15 +968,17 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   s->K = K; s->G = groups; s->F = (int)F; s->B = B; s->model = model;
   s->order_mode = opt.order_mode;
   s->shard = opt.shard_rank; s->nshard = opt.shard_count;
-  // column shards: exchanges per sweep E.  0 (default) = automatic: E = the shard count, at most the
-  // blocks per shard -- global quantities, so every shard runs the same E (the exchange is a
-  // collective).  One segment's stale residual of the other S - 1 shards is then (S - 1) / S^2 of a
-  // sweep's changes; 8 shards at E = 8 pass the distributional test against the 1-shard chain where
-  // E = 1 is biased by +2.9 % in sigmaE.
+  // column shards: exchanges per sweep E.  0 (default) = automatic: E = 8, at most the blocks per
+  // shard -- global quantities, so every shard runs the same E (the exchange is a collective).  A
+  // segment's stale residual of the other S - 1 shards is then (S - 1) / (S E) < 1/8 of a sweep's
+  // changes; the sigmaE bias grows about linearly in that fraction (+3.0 % at 8 shards and E = 1, +0.7 %
+  // at 2 shards and E = 2, +0.13 % at 8 shards and E = 8: profiles/r03_shard_bias.jsonl,
+  // profiles/r04_shard_bias_E_eq_S.jsonl), and 8 shards at E = 8 pass the distributional test against
+  // the 1-shard chain.
   if (s->nshard > 1) {
     const int64_t nbt = (M_total + B - 1) / B;
     s->nex = opt.exchanges_per_sweep > 0 ? opt.exchanges_per_sweep
-                                         : (int)std::max<int64_t>(1, std::min<int64_t>(s->nshard, nbt / s->nshard));
+                                         : (int)std::max<int64_t>(1, std::min<int64_t>(8, nbt / s->nshard));
   } else {
     s->nex = 1;
   }

@@ -1,7 +1,7 @@
 """Column-sharded multi-GPU driver helpers: one process per GPU, markers split
 into contiguous ranges of whole blocks, the residual kept coherent by ONE all-reduce of the
 residual deltas (and the marker statistics) per exchange segment: brr_options.exchanges_per_sweep =
-E rounds per sweep (default: E = the shard count; 1 = one exchange per sweep).
+E rounds per sweep (default: E = 8, at most the blocks per shard; 1 = one exchange per sweep).
 
 Two exchange paths share the same session protocol (brr_session_sweep_local -> sum ->
 brr_session_sweep_finish):

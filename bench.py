@@ -134,9 +134,9 @@ def parse():
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-roofline-events", action="store_true")
     ap.add_argument("--exchanges", type=int, default=0,
-                    help="column shards: residual exchanges per sweep E (0 = the library's automatic E = the shard "
-                         "count, whose 8-shard chain matches the 1-shard chain; 1 = north_star's one all-reduce per "
-                         "sweep, biased from 2 shards on; DESIGN.md section 9)")
+                    help="column shards: residual exchanges per sweep E (0 = the library's automatic E = 8, whose "
+                         "8-shard chain matches the 1-shard chain; 1 = north_star's one all-reduce per sweep, "
+                         "biased from 2 shards on; DESIGN.md section 9)")
     ap.add_argument("--rank-of", type=int, default=0, metavar="S",
                     help="measurement: time ONE rank's real workload of an S-GPU column-sharded job on this GPU "
                          "(shard 0 of S, every exchange segment, BRR_EXCHANGE_LOOPBACK=1: the other ranks' deltas "

@@ -85,9 +85,10 @@ typedef struct brr_options {
    * E segments of whole blocks (segment e = blocks [nb e / E, nb (e + 1) / E)); after every segment
    * the residual deltas are summed across the shards, so a shard sees the other shards' changes at
    * most one segment late instead of one sweep (stale-residual bias).
-   * 0 (default) = automatic: E = shard_count, capped at ceil(M_total / B) / shard_count -- the
-   * setting whose 8-shard chain matches the 1-shard chain within Monte-Carlo error.  1 = north_star's
-   * single exchange per sweep (measurably biased from 2 shards on).  Every shard must use the same E.
+   * 0 (default) = automatic: E = 8, capped at ceil(M_total / B) / shard_count -- a shard then sees
+   * less than 1/8 of a sweep's changes of the others late, and the 8-shard chain matches the 1-shard
+   * chain within Monte-Carlo error.  1 = north_star's single exchange per sweep (measurably biased
+   * from 2 shards on).  Every shard must use the same E.
    * Ignored without column shards. */
   int32_t exchanges_per_sweep;
 } brr_options;

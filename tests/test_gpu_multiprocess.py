@@ -44,7 +44,7 @@ def test_two_processes_column_shards(oracle_mod, require_gpu, tmp_path, model, o
     kw = dict(cva=CVA, **HYP) if model == O.V2 else dict(A=0.01, v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0,
                                                         c2=1.0, vC=10.0, sC=10.0)
     E = int(np.load(tmp_path / "E0.npy")[0])
-    assert E == 2 and int(np.load(tmp_path / "E1.npy")[0]) == E  # automatic: the shard count, same on every rank
+    assert E == 2 and int(np.load(tmp_path / "E1.npy")[0]) == E  # automatic: 8 capped at 5 blocks / 2 shards, same on every rank
     ref = O.Oracle(model, X, Y, seed=9, order_mode=order, block_size=B, n_shards=world, n_exchanges=E, **kw)
     ref.sweep(4)
     beta = np.concatenate([np.load(tmp_path / f"beta{r}.npy") for r in range(world)])
