@@ -261,7 +261,9 @@ int run_chain(brr_session *s, const Run &r, CsvWriter *w) {
       }
     }
     const auto ta = std::chrono::steady_clock::now();
-    if (int rc = brr_session_sweep(s, 1)) return rc;
+    // the device error check (stream sync + read-back) every 16 iterations and at the end: a per-sweep
+    // sync left the device idle for the host's launches of every sweep (C1: 7.4 against 6.9 ms)
+    if (int rc = brr::session_sweep(s, 1, (it & 15) == 15 || it + 1 == r.max_it)) return rc;
     const auto tb = std::chrono::steady_clock::now();
     t_sweep += std::chrono::duration<double, std::milli>(tb - ta).count();
     if (it >= r.burn_in && it % r.thin == 0) {

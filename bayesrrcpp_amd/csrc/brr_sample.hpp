@@ -34,6 +34,11 @@ void sample_ring_release(brr_session *s, int slot);
 void sample_ring_close(brr_session *s);
 int sample_ring_max_in_use(brr_session *s);  // diagnostics: most slots ever taken at once
 
+// n sweeps as brr_session_sweep (single-GPU sessions), with the device error check (a stream sync and
+// a read-back of the hand-over words) only when `check` is set: the one-shots check every few
+// iterations instead of after each sweep, so the host keeps the device queue full
+int session_sweep(brr_session *s, int n, bool check);
+
 // a caller's options over the defaults, by the caller's ABI version: an older caller's struct
 // ends before the fields a later ABI added (ABI 1: row shards, ABI 2: exchanges_per_sweep)
 brr_options options_from_caller(const brr_options *in);

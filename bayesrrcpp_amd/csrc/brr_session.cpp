@@ -1547,7 +1547,11 @@ int brr_session_init_finish(brr_session *s) {
   return init_finish(s, s->ex_stats);
 }
 
-int brr_session_sweep(brr_session *s, int32_t n) {
+int brr_session_sweep(brr_session *s, int32_t n) { return brr::session_sweep(s, n, true); }
+
+}  // extern "C"
+
+int brr::session_sweep(brr_session *s, int n, bool check) {
   if (!s) return -1;
   if (s->nrshard > 1) {
     Coll c{{s}};
@@ -1592,8 +1596,10 @@ int brr_session_sweep(brr_session *s, int32_t n) {
       if (int rc = do_sweep_finish(s)) return rc;
     }
   }
-  return check_device_error(s);
+  return check ? check_device_error(s) : 0;
 }
+
+extern "C" {
 
 int brr_comm_unique_id(void *out) {
   if (!out) return -1;

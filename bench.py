@@ -414,6 +414,13 @@ def main():
                       block_size=Bsz, order_mode=order_mode, shard_rank=srank, shard_count=nshard,
                       x_storage=L.X_2BIT if x2 else L.X_F32, exchanges_per_sweep=args.exchanges)
     n_ex = s.exchanges_per_sweep
+
+    def diag_scalar(k, default=0):
+        """a diagnostic scalar of the library (not in brr.h); an older library build lacks some"""
+        try:
+            return s.scalar(k)
+        except Exception:  # noqa: BLE001 -- older libbrr (A/B runs): the field is absent
+            return default
     # algorithmic bytes of one pass over this shard's genotypes (f32 values, or 2-bit codes + the
     # 16-B value table of every column)
     x_bytes = (Nl * Pl / 4.0 + 16.0 * Pl) if x2 else 4.0 * Nl * Pl
@@ -488,8 +495,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms = dt / args.steps * 1e3
-    if s.scalar(130) > 0:  # the fused sweep fell back to the per-block kernels: say so, loudly
-        print(f"bench.py: WARNING: {int(s.scalar(130))} fused sweep(s) failed the residency census; the "
+    if diag_scalar(130) > 0:  # the fused sweep fell back to the per-block kernels: say so, loudly
+        print(f"bench.py: WARNING: {int(diag_scalar(130))} fused sweep(s) failed the residency census; the "
               "session ran the per-block kernels afterwards (see config.census_failures)", file=sys.stderr)
     diag = {"slow_steps_per_sweep": s.scalar(100) / (args.warmup + args.steps),
             "changed_per_sweep": s.scalar(101) / (args.warmup + args.steps),
@@ -595,8 +602,8 @@ def main():
                      + ("2-bit codes + f32 value tables" if x2 else "f32 X") + ", f64 arithmetic)"),
             "config": {"workload": cfg["workload"] + (" [2-bit genotype storage, SURVEY 8f3]" if x2 else ""),
                        "x_storage": args.x_storage, "N": N, "P": P, "K": K, "groups": G,
-                       "block_size": Bsz, "order": args.order, "fused_stream_wg": int(s.scalar(104)), "code_cache": int(s.scalar(105)), "pipeline_lag": int(s.scalar(106)), "stream_wg_threads": int(s.scalar(109)),
-                       "census_failures": int(s.scalar(130)),
+                       "block_size": Bsz, "order": args.order, "fused_stream_wg": int(s.scalar(104)), "code_cache": int(s.scalar(105)), "pipeline_lag": int(s.scalar(106)), "stream_wg_threads": int(diag_scalar(109)),
+                       "census_failures": int(diag_scalar(130)),
                        "parallelism": (f"row-shard x{world} (exact)" if rows
                                        else f"column-shard rank 0 of {emu} emulated on 1 GPU, {n_ex} exchanges per sweep "
                                             f"(other ranks' deltas zero, no collective; a per-rank rate, not a whole-job one)"
