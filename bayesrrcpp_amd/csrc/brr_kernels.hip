@@ -146,11 +146,25 @@ __device__ __forceinline__ double ld_sc1(const double *p) {
   return __longlong_as_double(__hip_atomic_load(reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT));
 }
+__device__ __forceinline__ unsigned long long ld_sc1_u64(const double *p) {
+  return __hip_atomic_load(reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1_u64(double *p, unsigned long long v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long *>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void st_sc1_int(int *p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ int ld_sc1_int(const int *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The persistent solver's hand-over of the reduced dots (slab2): a slot holds the sentinel of the block
+// that will use it next until its reducer overwrites it with the dot -- a signalling-NaN bit pattern
+// that arithmetic never produces (it yields quiet NaNs), carrying the block's session-wide epoch
+// (Dev::sbase + s) so that a stale value of an earlier block is never mistaken for ready data.
+__host__ __device__ inline unsigned long long slab_sentinel(int epoch) {
+  return 0x7FF4000000000000ull | (unsigned long long)(unsigned)epoch;
 }
 
 // Bounded wait (one lane) for a device counter published by a kernel running concurrently on
@@ -2398,9 +2412,11 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     chain_coefficients<B, NT>(slots, Linv, Lposg);
   }
   const uint64_t tA3 = prof ? wall_clock64() : 0;  // coefficients built
-  // B) wait for k_stream(s)'s reduction groups (other queue; cumulative count)
+  // B) wait for k_stream(s)'s reduction groups (other queue; cumulative count).  The persistent
+  // solver instead polls the reduced dots themselves in step 1 (each slot holds this block's
+  // sentinel until its reducer writes it): one HBM round trip less than counter, barrier and loads.
   if (t == 0 && s == 0) stamp(d.sync, 3);
-  if (t == 0) wait_geq(d.sync + SY_GDONE + 32 * par, (d.gbase[par] + s / NPAR + 1) * d.gtarget, d.sync, 3);
+  if (t == 0 && !persistent) wait_geq(d.sync + SY_GDONE + 32 * par, (d.gbase[par] + s / NPAR + 1) * d.gtarget, d.sync, 3);
   if (t == 0 && s == 0) stamp(d.sync, 4);
   if (defer_dma) {
     lds_barrier();  // (the copying waves wait for their pieces just before the chain)
@@ -2423,18 +2439,40 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   for (int c = 0; c < NPT; ++c) {
     const int pos = t + NT * c;
     bool likely = false;
-    if (pos < bs) {
-      double dsum = 0.0;
+    double dsum = 0.0;
+    // (persistent solver) every one of the B slot columns is polled by one thread -- a short last
+    // block's unread columns too -- so that no reducer store can land after the sentinel stores below
+    if (pos < bs || (persistent && pos < B)) {
       // the dots are by visit position, or by in-block (storage) index when the 2-bit streamers
-      // read the block in storage order
-      const int sidx = d.slab_storage ? Lgi[pos] : pos;
+      // read the block in storage order (a permutation of 0 .. bs-1; columns bs .. B-1 are unread)
+      const int sidx = pos < bs && d.slab_storage ? Lgi[pos] : pos;
+      const unsigned long long sent = slab_sentinel(d.sbase + s);
       for (int g0 = 0; g0 < d.NG; g0 += 16) {
-        double v[16];
+        unsigned long long v[16];
+        for (uint32_t n = 0;; ++n) {
+          bool ready = true;
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = g0 + u < d.NG ? ld_sc1(slab2 + (int64_t)(g0 + u) * B + sidx) : 0.0;
+          for (int u = 0; u < 16; ++u) {
+            v[u] = g0 + u < d.NG ? ld_sc1_u64(slab2 + (int64_t)(g0 + u) * B + sidx) : 0ull;
+            ready = ready && (!persistent || v[u] != sent);
+          }
+          if (ready) break;
+          if (n > SPIN_MAX) {  // bounded, as wait_geq: the host reports the protocol error
+            if (atomicCAS(d.sync + SY_ERR, 0, 1) == 0) {
+              st_sc1_int(d.sync + SY_ERR + 1, 3);
+              st_sc1_int(d.sync + SY_ERR + 2, d.sbase + s);
+              st_sc1_int(d.sync + SY_ERR + 3, g0);
+              st_sc1_int(d.sync + SY_ERR + 4, (int)blockIdx.x);
+            }
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
 #pragma unroll
-        for (int u = 0; u < 16; ++u) dsum += v[u];
+        for (int u = 0; u < 16; ++u) dsum += __longlong_as_double((long long)v[u]);
       }
+    }
+    if (pos < bs) {
       const double bo = Lbo[pos], x2 = Lx2[pos];
       // num = x.(eps + x b_old) (BayesRv2.cpp:191-193), x.eps = d - cross-Gram correction
       const double r = (dsum - Lr0[pos]) + x2 * bo;
@@ -2471,6 +2509,15 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     }
     for (int w = 0; w < NW; ++w) base += misc[w];
     if (defer_dma) lds_barrier(); else __syncthreads();
+  }
+  if (persistent) {
+    // every position has read this block's dots (barrier above): the slots get the sentinel of the
+    // next block that uses them -- s + NPAR in this sweep, else block s % NPAR of the next sweep (its
+    // reducer can only write after this solver publishes later blocks, so these stores land first)
+    const int nxt = s + NPAR < d.nb ? d.sbase + s + NPAR : d.sbase + d.nb + s % NPAR;
+    const unsigned long long ns = slab_sentinel(nxt);
+    double *slab2w = d.slab2 + par * d.slab2_stride;
+    for (int i = t; i < d.NG * B; i += NT) st_sc1_u64(slab2w + i, ns);
   }
   const int nused = resident ? 0 : min(base, nst);  // resident: every row is in LDS already
   const int nov = max(base - nst, 0);  // predicted positions served by the ring
@@ -4216,6 +4263,19 @@ hipError_t set_solve_lds_limit(int /*B*/) {
 
 hipError_t launch_linpred(const Dev &d, double *out, hipStream_t st) {
   hipLaunchKernelGGL(k_linpred, dim3(cdiv64(d.N, 256)), dim3(256), 0, st, d, out);
+  return hipGetLastError();
+}
+
+__global__ void k_slab_sentinels(double *slab2, int64_t stride, int nrow, int B, int epoch0) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int p = blockIdx.y;
+  if (i < (int64_t)nrow * B) reinterpret_cast<unsigned long long *>(slab2 + p * stride)[i] = slab_sentinel(epoch0 + p);
+}
+// the persistent solver's slab2 slots before the session's first fused sweep: slot p holds block p's
+// sentinel (epoch p); nrow = the padded row count (all of them)
+hipError_t launch_slab_sentinels(const Dev &d, int nrow, hipStream_t st) {
+  hipLaunchKernelGGL(k_slab_sentinels, dim3(cdiv64((int64_t)nrow * d.B, 256), NPAR), dim3(256), 0, st, d.slab2,
+                     d.slab2_stride, nrow, d.B, 0);
   return hipGetLastError();
 }
 

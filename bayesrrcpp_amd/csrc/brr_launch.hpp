@@ -55,6 +55,7 @@ hipError_t launch_solve(const Dev &d, int s, uint32_t it, hipStream_t st);
 hipError_t set_solve_lds_limit(int B);
 size_t solve_lds_bytes(int B, int K);
 hipError_t launch_linpred(const Dev &d, double *out, hipStream_t st);
+hipError_t launch_slab_sentinels(const Dev &d, int nrow, hipStream_t st);  // fused solver's dot slots (epoch p in slot p)
 hipError_t launch_markers(const Dev &d, int mode, uint32_t it, hipStream_t st);
 hipError_t launch_hyper(const Dev &d, uint32_t it, const double *stats, hipStream_t st);
 hipError_t launch_hyper_init(const Dev &d, const double *stats, bool pi_given, hipStream_t st);

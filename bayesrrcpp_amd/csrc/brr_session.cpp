@@ -327,6 +327,8 @@ int check_device_error(brr_session *s, bool mid_sweep = false) {
       const int NC = s->B >= 128 ? s->B / 128 : 1;
       HIPCHK(hipMemset(s->d.sync, 0, sizeof(int) * SY_WORDS));
       HIPCHK(hipMemset(s->d.cnt1, 0, sizeof(int) * NPAR * s->d.NG * NC));
+      // the per-block solve sums whole padded batches of slab2 rows: no fused-solver sentinels left
+      HIPCHK(hipMemset(s->d.slab2, 0, sizeof(double) * NPAR * s->d.slab2_stride));
       // The sweep's remaining segments (exchange segments, from block position f1 on) run on the
       // per-block kernels with this sweep's epoch bases (Dev::sbase / gbase, set at segment 0):
       // rebase them so that the counters, now zero, read as if blocks [0, f1) had passed, and the
@@ -1135,6 +1137,13 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     if (rows || ref2bit || (pb && pb[0] == '1') || !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused, f32cc))
       s->fused = FusedCfg{};
     if (s->fused.nsg == 0) d.lag = 1;
+    // the persistent solver polls its reduced dots against per-block sentinels (brr_kernels.hip
+    // slab_sentinel): slot p starts with block p's
+    if (s->fused.nsg > 0 && launch_slab_sentinels(d, (int)(d.slab2_stride / B), s->st) != hipSuccess) {
+      set_error("cannot initialise the dot slots");
+      delete s;
+      return nullptr;
+    }
     // lag 1 while the solver bounds the sweep: more than ~15 changed markers per block at C2's
     // 100,000 rows (measured crossover of the burn-in sweeps at B = 512; round 3, after the
     // streamers' list prefetch and the row chain's typed loads: sweeps 5-24 at 34.01 / 34.14 ms
