@@ -372,6 +372,10 @@ def main():
             sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to time a mislabelled run")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.config == "c5" and world == 1 and args.rank_of <= 1:
+        # C5's 2 TB of f32 genotypes need 8 GPUs: on one GPU, time one rank's real share of it
+        print("bench.py: --config c5 on one GPU times rank 0 of 8 (--rank-of 8)", file=sys.stderr)
+        args.rank_of = 8
     emu = args.rank_of if world == 1 and args.rank_of > 1 else 0  # one rank of an emu-GPU job, emulated
     if emu:
         os.environ["BRR_EXCHANGE_LOOPBACK"] = "1"
