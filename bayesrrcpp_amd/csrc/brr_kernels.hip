@@ -1665,7 +1665,7 @@ __device__ __forceinline__ int sweep_lag(const Dev &d) { return d.sc->lag_next >
 // nlb: change-list buffers kept in LDS from block to block (persistent solver: one per pipeline lag,
 // block s's list in buffer s % nlb, each B + 16 doubles of deltas and B + 16 Gram indices)
 __host__ __device__ inline size_t solve_fixed_bytes(int B, int K, int nlb = 0) {
-  return (size_t)(10 + K + (K > 1 ? K - 1 : 0)) * 8 * B + (size_t)6 * 4 * B + 128 + (size_t)nlb * 12 * (B + 16);
+  return (size_t)(11 + K + (K > 1 ? K - 1 : 0)) * 8 * B + (size_t)6 * 4 * B + 128 + (size_t)nlb * 12 * (B + 16);
 }
 constexpr size_t SOLVE_LDS_MAX = 160 * 1024;
 // phase A scratch in the slot area (doubles): the change list (deltas, gram indices) and the
@@ -1981,7 +1981,7 @@ __device__ __forceinline__ void chain_bayesr_resident(const Dev &d, int bs, doub
 template <int B>
 __device__ __forceinline__ void chain_bayesr_rows(const Dev &d, int bs, double sigmaE, const double *Lr0,
                                                   const double *Llo, const double *Lhi, double *Ldsel, double *Lsdz,
-                                                  const double *Lbo, double *Lbn, int *Lfl, int *Lks, const int *Lgi,
+                                                  double *Linv, const double *Lbo, double *Lbn, int *Lfl, int *Lks, const int *Lgi,
                                                   const double *La, const double *Lden, const double *Lp,
                                                   const double *Lx2, const double *Lz, const int *Lm, const int *Lslot,
                                                   const int *Lspos, const double *slots, const double *Ggl, int RS,
@@ -2020,13 +2020,15 @@ __device__ __forceinline__ void chain_bayesr_rows(const Dev &d, int bs, double s
     // this lane's lowest candidate: its constants and its new beta (the fast arm)
     const int posl = min(lane * NS + ql, bs - 1);
     const int fll = Lfl[posl];
-    const double dsl = Ldsel[posl], szl = Lsdz[posl], bol = Lbo[posl];
+    const double dsl = Ldsel[posl], ivl = Linv[posl], szl = Lsdz[posl], bol = Lbo[posl];
     const int sll = Lslot[posl];
     double rv = r[0];
 #pragma unroll
     for (int q = 1; q < NS; ++q) rv = ql == q ? r[q] : rv;
     const int ksl = fll & 0xFF;
-    const double bnl = ksl == 0 ? 0.0 : (ksl == FALLTHROUGH ? bol : rv / dsl + szl);  // BayesRv2.cpp:226-230
+    // BayesRv2.cpp:226-230; num / D as q0 = num RN(1/D) plus one exact-remainder correction (the
+    // resident chain's quotient): three dependent operations on the step's path instead of a division
+    const double bnl = ksl == 0 ? 0.0 : (ksl == FALLTHROUGH ? bol : quot_rn(rv, dsl, ivl) + szl);
     const int fastl = (int)((win >> ql) & 1u) & (int)((fll & PF_EX) == 0);
     const uint64_t bal = __ballot(cand != 0);
     if (!bal) break;  // the rest keep their decisions (no change)
@@ -2052,6 +2054,7 @@ __device__ __forceinline__ void chain_bayesr_rows(const Dev &d, int bs, double s
           Lfl[first] = (o.k & 0xFF) | (o.ex ? PF_EX : 0) | (lk ? PF_LIKELY : 0);
           Lks[first] = o.k;
           Ldsel[first] = dsel;
+          Linv[first] = 1.0 / dsel;
           Lsdz[first] = sqrt(sigmaE / dsel) * Lz[first];
         }
         if (lane == L) {
@@ -2191,7 +2194,9 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   const int K = HS ? 1 : d.K;
   const int KD = K > 1 ? K - 1 : 0;
   double *Lr0 = reinterpret_cast<double *>(smem);
-  double *Llo = Lr0 + B, *Lhi = Llo + B, *Ldsel = Lhi + B, *Lsdz = Ldsel + B, *Lbo = Lsdz + B, *Lbn = Lbo + B,
+  // (Linv: 1 / D of each position's decision, for the row chain's quotient; Lbo .. Lden stay contiguous
+  // for the constants' LDS-DMA)
+  double *Llo = Lr0 + B, *Lhi = Llo + B, *Ldsel = Lhi + B, *Lsdz = Ldsel + B, *Linv = Lsdz + B, *Lbo = Linv + B, *Lbn = Lbo + B,
          *Lx2 = Lbn + B, *Lp = Lx2 + B, *Lz = Lp + B, *La = Lz + B, *Lden = La + (int64_t)K * B;
   int *Lfl = reinterpret_cast<int *>(Lden + (int64_t)KD * B);
   int *Lks = Lfl + B, *Lgi = Lks + B, *Lm = Lgi + B, *Lslot = Lm + B, *Lspos = Lslot + B, *misc = Lspos + B;
@@ -2493,6 +2498,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       Llo[pos] = o.lo;
       Lhi[pos] = o.hi;
       Ldsel[pos] = dsel;
+      Linv[pos] = 1.0 / dsel;
       Lsdz[pos] = sqrt(sigmaE / dsel) * Lz[pos];  // rnorm(muk, sqrt(sigmaE/denom)) noise
       if (HS) Lp[pos] = 1.0 / dsel;                 // RN(1/D) for the chain's quotient
     }
@@ -2655,7 +2661,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     if (lane == 0) lds_st_rel(Lcons, RING_DONE);
     if (prof && lane == 0) atomicAdd(&d.sc->prof[6], (unsigned long long)bs);
   } else if (!HS && t < 64) {
-    chain_bayesr_rows<B>(d, bs, sigmaE, Lr0, Llo, Lhi, Ldsel, Lsdz, Lbo, Lbn, Lfl, Lks, Lgi, La, Lden, Lp, Lx2, Lz, Lm,
+    chain_bayesr_rows<B>(d, bs, sigmaE, Lr0, Llo, Lhi, Ldsel, Lsdz, Linv, Lbo, Lbn, Lfl, Lks, Lgi, La, Lden, Lp, Lx2, Lz, Lm,
                          Lslot, Lspos, slots, d.gram + (int64_t)gb * B * B, RS, nst, nov, Lcons, Lready, prof);
     if (prof) tce = wall_clock64();
   } else if (RS > 0 && nov > 0) {
