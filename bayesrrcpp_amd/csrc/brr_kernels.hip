@@ -1985,7 +1985,7 @@ __device__ __forceinline__ void chain_bayesr_rows(const Dev &d, int bs, double s
                                                   const double *La, const double *Lden, const double *Lp,
                                                   const double *Lx2, const double *Lz, const int *Lm, const int *Lslot,
                                                   const int *Lspos, const double *slots, const double *Ggl, int RS,
-                                                  int nst, int nov, int *Lcons, int *Lready, bool prof) {
+                                                  int nst, int nov, int npred, int *Lcons, int *Lready, bool prof) {
 #pragma clang fp contract(off)
   constexpr int NS = B / 64;
   constexpr uint32_t ALLQ = NS >= 32 ? 0xFFFFFFFFu : ((1u << NS) - 1u);
@@ -2009,6 +2009,14 @@ __device__ __forceinline__ void chain_bayesr_rows(const Dev &d, int bs, double s
   }
   int nslow = 0, nsteps = 0, nref = 0, nglob = 0;
   int kc = 0;  // ring cursor: entries below kc are released
+  // the Gram row of the next predicted position with a static slot (Lspos[kp], kp < nsp), gathered one
+  // step ahead -- before this step's update -- so that a step that visits it finds the row in
+  // registers (its LDS latency off the step's dependency chain).  B = 256 only: at B = 512 its NS more
+  // live registers spill in the solver kernel (C1 146 -> 152 sweeps/s; C2 30.2 -> 28.4 with it at 512)
+  constexpr bool PREF = B <= 256;
+  const int nsp = PREF ? min(npred, nst) : 0;
+  int kp = 0, pre = -1;
+  double gpre[NS];
   uint64_t tref = 0;
   const uint64_t tl0 = prof ? wall_clock64() : 0;
   int i = 0;
@@ -2096,7 +2104,10 @@ __device__ __forceinline__ void chain_bayesr_rows(const Dev &d, int bs, double s
       // below then became NS branches, each a FLAT load and a full vmcnt / lgkmcnt wait: ~3,300
       // shader clocks per step at B = 512), all issued before any is used
       double g[NS];
-      if (lrow >= 0) {
+      if (PREF && first == pre) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) g[q] = gpre[q];
+      } else if (lrow >= 0) {
         const __attribute__((address_space(3))) double *row =
             (const __attribute__((address_space(3))) double *)(slots + (int64_t)lrow * B);
 #pragma unroll
@@ -2106,6 +2117,16 @@ __device__ __forceinline__ void chain_bayesr_rows(const Dev &d, int bs, double s
             (const __attribute__((address_space(1))) double *)(Ggl + (int64_t)Lgi[first] * B);
 #pragma unroll
         for (int q = 0; q < NS; ++q) g[q] = row[gg[q]];
+      }
+      // the next predicted position's row, in flight during this step's update
+      while (PREF && kp < nsp && __builtin_amdgcn_readfirstlane(Lspos[kp]) <= first) ++kp;
+      pre = -1;
+      if (PREF && kp < nsp) {
+        pre = __builtin_amdgcn_readfirstlane(Lspos[kp]);
+        const __attribute__((address_space(3))) double *row =
+            (const __attribute__((address_space(3))) double *)(slots + (int64_t)__builtin_amdgcn_readfirstlane(Lslot[pre]) * B);
+#pragma unroll
+        for (int q = 0; q < NS; ++q) gpre[q] = row[gg[q]];
       }
 #pragma unroll
       for (int q = 0; q < NS; ++q) asm volatile("" ::"v"(g[q]));  // every load lands before the update
@@ -2181,12 +2202,11 @@ __device__ __attribute__((noinline)) void chain_bayesr_call(
 #ifndef BRR_EARLY_GRAM
 #define BRR_EARLY_GRAM 0
 #endif
+
 // persistent: one workgroup solves every block of the sweep in order (LDS persists between blocks)
 template <bool HS, int B, int NT>
-// gi_pref: (persistent) the Gram index of position threadIdx.x % B of the next block, loaded one
-// block ahead so the next block's cross-Gram loads need no dependent round trip
 __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, int nslot, char *smem,
-                                            bool persistent, int &gi_pref, int lag) {
+                                            bool persistent, int lag) {
 #pragma clang fp contract(off)
   constexpr int NPT = (B + NT - 1) / NT;  // positions per thread, parallel phases
   constexpr int NW = NT / 64;             // waves
@@ -2226,10 +2246,6 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     for (int j = 0; j < LAG_MAX; ++j) misc[17 + 2 * j] = -2;
   }
   const bool pipelined = persistent && resident;
-  // the Gram index of this thread's position, loaded one block ahead by the persistent solver
-  const bool prefgi = persistent && NPT == 1;
-  const int gi_t = (prefgi && s > d.seg0) ? gi_pref : (t % B < bs ? d.gidx[q0 + t % B] : 0);
-  if (prefgi && s + 1 < d.seg1) gi_pref = d.gidx[(int64_t)(s + 1) * B + t % B];
 
   // A) everything that does not depend on k_stream(s): the per-position constants, the cross-Gram
   // correction for the changes of the blocks the streamed dots have not seen, and (resident mode) the
@@ -2242,6 +2258,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   // waves 0 .. NW/2-1 load the constants and form the correction; otherwise every wave does both (the
   // Horseshoe's coefficient pass needs the Gram block before the wait).
   const bool defer_dma = pipelined && !HS;
+
   const int dma_w0 = defer_dma ? NW / 2 : 0;  // first wave of the Gram copy
   const int cw1 = defer_dma ? NW / 2 : NW;    // waves [0, cw1) load the constants
   {
@@ -2337,13 +2354,18 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     }
   }
   if (staged) __syncthreads();
+  // The sums are formed per Gram index j of block s (the columns of a cross-Gram row are Gram
+  // indices, so a wave's 64 loads of one entry are 512 contiguous bytes; by visit position they were
+  // 64 scattered ones) into Lcor[j] (the correction of the position whose Gram index is j, read by
+  // the decisions through Lgi); per j the same operations in the same order as by position.
+  double *Lcor = Lpart;
 #pragma unroll
   for (int c = 0; c < NPT; ++c) {
-    const int pos = (t % (B < NT ? B : NT)) + NT * c;
+    const int pos = (t % (B < NT ? B : NT)) + NT * c;  // (here: the Gram index j)
     const int grp = B < NT ? t / B : 0;
     double corr[LAG_MAX] = {0.0, 0.0, 0.0};
     if (pos < bs && grp < PG) {
-      const int gi = NPT == 1 ? gi_t : d.gidx[q0 + pos];  // (Lgi is still in flight)
+      const int gi = pos;
       int c0[LAG_MAX], c1[LAG_MAX];
 #pragma unroll
       for (int l = 0; l < LAG_MAX; ++l) {
@@ -2382,11 +2404,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     }
     // the lists' sums added in list order (per thread group, then the groups in group order)
     const double tot = (corr[0] + corr[1]) + corr[2];
-    if (PG == 1) {
-      if (pos < bs && grp == 0) Lr0[pos] = tot;
-    } else if (grp < PG) {
-      Lpart[grp * B + pos] = tot;
-    }
+    if (grp < PG) Lcor[grp * B + pos] = tot;
   }
   // the constant-loading waves' LDS-DMA has landed before any wave reads the constants (the
   // deferred Gram copy's waves wait for theirs just before the chain)
@@ -2396,7 +2414,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     if (t < bs) {
       double tot = Lpart[t];
       for (int g = 1; g < PG; ++g) tot += Lpart[g * B + t];
-      Lr0[t] = tot;
+      Lcor[t] = tot;
     }
   }
   const uint64_t tA2 = prof ? wall_clock64() : 0;  // cross-Gram correction done
@@ -2480,7 +2498,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     if (pos < bs) {
       const double bo = Lbo[pos], x2 = Lx2[pos];
       // num = x.(eps + x b_old) (BayesRv2.cpp:191-193), x.eps = d - cross-Gram correction
-      const double r = (dsum - Lr0[pos]) + x2 * bo;
+      const double r = (dsum - Lcor[Lgi[pos]]) + x2 * bo;
       FastDec o;
       double dsel;
       if (HS) {
@@ -2662,7 +2680,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     if (prof && lane == 0) atomicAdd(&d.sc->prof[6], (unsigned long long)bs);
   } else if (!HS && t < 64) {
     chain_bayesr_rows<B>(d, bs, sigmaE, Lr0, Llo, Lhi, Ldsel, Lsdz, Linv, Lbo, Lbn, Lfl, Lks, Lgi, La, Lden, Lp, Lx2, Lz, Lm,
-                         Lslot, Lspos, slots, d.gram + (int64_t)gb * B * B, RS, nst, nov, Lcons, Lready, prof);
+                         Lslot, Lspos, slots, d.gram + (int64_t)gb * B * B, RS, nst, nov, npred, Lcons, Lready, prof);
     if (prof) tce = wall_clock64();
   } else if (RS > 0 && nov > 0) {
     ring_produce<B, NW>(d.gram + (int64_t)gb * B * B, Lgi, Lspos, nst, nov, slots + (int64_t)nst * B, RS, Lcons,
@@ -2783,8 +2801,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
 template <bool HS, int B>
 __global__ __launch_bounds__(256) void k_solve(Dev d, int s, uint32_t it, int nslot) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  int gi_pref = 0;
-  solve_block<HS, B, 256>(d, s, it, nslot, smem, false, gi_pref, d.lag);
+  solve_block<HS, B, 256>(d, s, it, nslot, smem, false, d.lag);
 }
 
 
@@ -3576,10 +3593,9 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
 #endif
 template <bool HS, int B, int NT = SWEEP_NT>
 __device__ BRR_SOLVER_INL void solver_role(const Dev &d, uint32_t it, int nslot, char *smem) {
-  int gi_pref = 0;
   const int lag = sweep_lag(d);
   for (int s = d.seg0; s < d.seg1; ++s) {
-    solve_block<HS, B, NT>(d, s, it, nslot, smem, true, gi_pref, lag);
+    solve_block<HS, B, NT>(d, s, it, nslot, smem, true, lag);
     __syncthreads();
   }
 }
