@@ -9,9 +9,10 @@ for rep in $(seq 1 ${REPS:-2}); do
   for cfg in ${CFGS:-c3:--config,c3 c2:--steps,20,--warmup,5}; do
     cname=${cfg%%:*}; cargs=$(echo ${cfg#*:} | tr ',' ' ')
     for v in ${VARIANTS:-head:}; do
-      vname=${v%%:*}; lib=${v#*:}
+      # name:library[:K=V] (empty library: the in-tree build; K=V: an environment variable for this variant)
+      IFS=: read -r vname lib venv <<< "$v"
       if [ -n "$lib" ]; then export BRR_LIB=$lib; else unset BRR_LIB; fi
-      timeout -k 10 240 python -u bench.py --no-cpu-baseline --no-roofline-events $cargs > gpurun_out/r4ab_${cname}_${vname}_$rep.log 2>&1 \
+      env $venv timeout -k 10 240 python -u bench.py --no-cpu-baseline --no-roofline-events $cargs > gpurun_out/r4ab_${cname}_${vname}_$rep.log 2>&1 \
         || { echo "$cname $vname FAILED"; tail -20 gpurun_out/r4ab_${cname}_${vname}_$rep.log; exit 1; }
       python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('$rep $cname $vname', d['value'], d['ms_per_step'])" gpurun_out/r4ab_${cname}_${vname}_$rep.log
     done
