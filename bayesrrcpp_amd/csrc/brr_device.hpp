@@ -102,6 +102,9 @@ struct Dev {
   int seg0, seg1;   // block positions of the current marker-loop launch(es): [seg0, seg1) (the
                     // sweep: [0, nb); a column-shard exchange segment: a part, brr_options)
   int gtarget;      // reduction groups k_solve(s) waits for (per-block: NG * NC; persistent: NG)
+  int ngr;          // (fused sweep) arrival groups of the streaming workgroups: the stride of cnt1
+  int rcorr;        // (fused sweep) the reducers subtract the cross-Gram corrections from the dots they
+                    // write (reduce_role); the solver's phase A then forms none
   int slab_storage; // the partial dots are indexed by in-block storage index, not visit position
                     // (fused sweep on 2-bit code tiles)
   uint64_t seed;

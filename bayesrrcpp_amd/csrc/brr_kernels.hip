@@ -780,23 +780,35 @@ __global__ __launch_bounds__(256) void k_gram_int(Dev d, const uint8_t *Xk, cons
     for (int u = 0; u < GI_D; ++u) {
       const int64_t ch = c0 + u;
       if (ch >= nch) break;
-      // expand: per column of the group, 4 rows' classes -> one 0/1 byte per row and plane
+      // expand: per column of the group, 4 rows' classes -> one 0/1 byte per row and plane.  Four
+      // columns at a time (a code word: byte = column, 2-bit field k = row k): the fields equal to
+      // class p are ~(w ^ p 0x55555555) with both bits set, kept as bit 2k of the column's byte; the
+      // bits 0, 2, 4, 6 of a byte y spread to bytes 0..3 as (y * 0x41041) & 0x01010101 (the partial
+      // products' other bits never carry into bits 0, 8, 16, 24)
 #pragma unroll
       for (int k = 0; k < EPT; ++k) {
         const int64_t row4 = ch * GI_KC + 4 * e_g[k];
-        const uint32_t vr = row4 >= N ? 0u : row4 + 4 <= N ? 0x01010101u : (0x01010101u >> (8 * (int)(4 - (N - row4))));
+        // valid rows of this quad as bits 0, 2, 4, 6 (row k: bit 2 k)
+        const uint32_t vrow = row4 >= N ? 0u : row4 + 4 <= N ? 0x55u : (0x55u >> (2 * (int)(4 - (N - row4))));
         const uint32_t cv = s_cv[e_side[k]][e_q[k]];
         const uint32_t wd[4] = {ring[u][k].x, ring[u][k].y, ring[u][k].z, ring[u][k].w};
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const uint32_t b = (wd[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-          const uint32_t cls = (b & 3u) | (b & 0xCu) << 6 | (b & 0x30u) << 12 | (b & 0xC0u) << 18;
-          const uint32_t valid = ((cv >> i) & 1u) ? vr : 0u;
-          uint8_t *dst = stg + (e_side[k] * NP * GI_T + 16 * e_q[k] + i) * GI_PITCH + 4 * e_g[k];
+        for (int j = 0; j < 4; ++j) {
+          // column validity (bytes) of columns 4 j .. 4 j + 3, times the row validity
+          const uint32_t cb = (cv >> (4 * j)) & 0xFu;
+          const uint32_t cm = ((cb & 1u) ? 0xFFu : 0u) | ((cb & 2u) ? 0xFF00u : 0u) | ((cb & 4u) ? 0xFF0000u : 0u) |
+                              ((cb & 8u) ? 0xFF000000u : 0u);
+          const uint32_t m = cm & (vrow * 0x01010101u);
 #pragma unroll
           for (int p = 0; p < NP; ++p) {
-            const uint32_t x = cls ^ (0x01010101u * (uint32_t)p);
-            *reinterpret_cast<uint32_t *>(dst + p * GI_T * GI_PITCH) = ~(x | (x >> 1)) & valid;
+            const uint32_t eq = ~(wd[j] ^ (0x55555555u * (uint32_t)p));
+            const uint32_t ind = eq & (eq >> 1) & m;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const uint32_t y = __builtin_amdgcn_ubfe(ind, 8 * c, 8);
+              uint8_t *dst = stg + (e_side[k] * NP * GI_T + 16 * e_q[k] + 4 * j + c) * GI_PITCH + 4 * e_g[k];
+              *reinterpret_cast<uint32_t *>(dst + p * GI_T * GI_PITCH) = (y * 0x41041u) & 0x01010101u;
+            }
           }
         }
       }
@@ -1653,8 +1665,8 @@ __device__ __forceinline__ int reduce16_col(int lane) {
 // counter) for k_stream(s)'s reduction groups, publishes block s's changes for k_solve(s+1)
 // and k_stream(s+2).
 // LDS layout (B positions):
-//   doubles  r0, lo, hi, dsel, sdz, bo, bn, x2, p, z [B each], a [K][B], den [K-1][B]
-//   ints     fl, ks, gi, m, slot, spos [B each], misc [16]
+//   doubles  r0, lo, hi, dsel, sdz, inv, bo, bn, x2, p, z [B each], a [K][B], den [K-1][B]
+//   ints     fl, ks, gi, m, slot, spos [B each], misc [32]; (persistent) nlb change lists
 //   slots    nslot Gram rows (B doubles each), staged for the positions predicted to change
 enum PrFlag : int { PF_EX = 1 << 8, PF_LIKELY = 1 << 9 };
 
@@ -2321,7 +2333,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
 #pragma unroll
   for (int l = 0; l < LAG_MAX; ++l) {
     const int sp = s - 1 - l;  // the earlier block
-    if (l >= nlist || sp < d.seg0) continue;
+    if (l >= nlist || sp < d.seg0 || (persistent && d.rcorr)) continue;  // (rcorr: the reducers subtract it)
     const int gp = d.gblk[sp];
     if (l == 0)
       Cl[l] = (gb == (gp + 1) % d.nb) ? d.xgram + (int64_t)gp * B * B : d.xgramT + (int64_t)gb * B * B;
@@ -3480,7 +3492,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     // per-wave arrivals measured 1.6x slower, contention on the group counters)
     __syncthreads();
     if (t == 0)
-      __hip_atomic_fetch_add(d.cnt1 + (s % NPAR) * d.NG + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(d.cnt1 + (s % NPAR) * d.ngr + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == 0) {
       if (prof) {
         tr_first(d, s, TR_ITEMS_FIRST);
@@ -3551,35 +3563,108 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
     if (r0 + i < r1) d.eps[r0 + i] = eps_l[i];
 }
 
-// Reducer workgroup r: for every block, the level-2 sums of the groups r, r + nred, ... (the
-// partials of a group's 16 streaming workgroups, in workgroup order) into slab2, then
-// one arrival on the solver's counter.  Kept off the streaming workgroups, which go straight on
-// to the next block.
+// Reducer workgroup r of nred: for every block, the whole sum over the nsg streaming workgroups'
+// partial dots of ITS columns [r cw, (r + 1) cw), cw = B / nred, into slab2 row 0 (the solver
+// reads one value per position).  Each of RED_NT logical threads sums a contiguous range of
+// workgroups for one column (in workgroup order); the RED_NT / cw ranges are added in range order
+// -- the same operations whatever the workgroup's width.  A column slice per reducer instead of a
+// group of streamers per reducer: every reducer reads nsg cw partials (C2: 196 x 16 doubles) rather
+// than a group's 64 B (256 KB at B = 512, ~9 us at one CU's share of HBM under the stream).
+// Dev::rcorr: the reducer also subtracts the column's cross-Gram corrections (the changes of blocks
+// s-1 .. s-lag, the solver's phase A sums, solve_block), each list's sum over RED_NT / cw contiguous
+// entry ranges added in range order, the lists as (c_1 + c_2) + c_3: the solver then reads corrected
+// dots and its phase A loads no cross-Gram rows (a C4 block's correction reads all 128 KB of its
+// cross-Gram block: at one CU's share of HBM that was half of the solver's phase A).
+constexpr int RED_NT = 512;
 template <int NT = SWEEP_NT>
-__device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nred, bool prof) {
+__device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nred, bool prof, double *s_red) {
+#pragma clang fp contract(off)
   const int t = threadIdx.x;
-  const int ng = (nsg + FUSED_GROUP - 1) / FUSED_GROUP;
   const int B = d.B;
+  const int cw = B / nred;            // columns of this reducer (a power of two, 8 .. RED_NT)
+  const int np = RED_NT / cw;         // workgroup ranges per column
+  const int cl = t % cw, part = t / cw;
+  const int w0 = part * nsg / np, w1 = (part + 1) * nsg / np;
+  const int col = r * cw + cl;
+  const int lag = sweep_lag(d);
+  double *s_ld = s_red + RED_NT;                            // a change list: deltas [B + 16]
+  int *s_lg = reinterpret_cast<int *>(s_ld + (B + 16));     // and Gram indices [B + 16]
   for (int s = d.seg0; s < d.seg1; ++s) {
     const int par = s % NPAR;
     const int use = d.gbase[par] + s / NPAR;
-    const double *slab1 = d.slab1 + par * d.slab1_stride;
-    for (int grp = r; grp < ng; grp += nred) {
-      const int gw0 = grp * FUSED_GROUP, gsz = min(FUSED_GROUP, nsg - gw0);
-      if (t == 0) wait_geq(d.cnt1 + par * d.NG + grp, (use + 1) * gsz, d.sync, 6);
-      __syncthreads();
-      for (int cl = t; cl < B; cl += NT) {
-        double v16[FUSED_GROUP];
+    const double *slab1 = d.slab1 + par * d.slab1_stride + col;
+    if (t == 0)
+      for (int grp = 0; grp < d.ngr; ++grp)
+        wait_geq(d.cnt1 + par * d.ngr + grp, (use + 1) * min(FUSED_GROUP, nsg - grp * FUSED_GROUP), d.sync, 6);
+    __syncthreads();
+    if (t < RED_NT) {
+      double acc = 0.0;
+      for (int w = w0; w < w1; w += 16) {
+        double v[16];
 #pragma unroll
-        for (int q = 0; q < FUSED_GROUP; ++q) v16[q] = q < gsz ? ld_sc1(slab1 + (int64_t)(gw0 + q) * B + cl) : 0.0;
-        double acc = 0.0;
+        for (int q = 0; q < 16; ++q) v[q] = w + q < w1 ? ld_sc1(slab1 + (int64_t)(w + q) * B) : 0.0;
 #pragma unroll
-        for (int q = 0; q < FUSED_GROUP; ++q) acc += v16[q];
-        st_sc1(d.slab2 + par * d.slab2_stride + (int64_t)grp * B + cl, acc);
+        for (int q = 0; q < 16; ++q)
+          if (w + q < w1) acc += v[q];
       }
-      publish_add(d.sync + SY_GDONE + 32 * par, 1);
-      if (prof && t == 0) { tr_first(d, s, TR_L2_FIRST); tr_last(d, s, TR_L2_LAST); }
+      s_red[part * cw + cl] = acc;
     }
+    __syncthreads();
+    double tot = 0.0;
+    if (t < cw) {
+      tot = s_red[t];
+      for (int p = 1; p < np; ++p) tot += s_red[p * cw + t];
+    }
+    if (d.rcorr && s > d.seg0) {
+      const int bs = d.bsz[s], gb = d.gblk[s];
+      // the column's Gram index (slab columns are visit positions, or storage indices = Gram indices)
+      const int gic = col < bs ? (d.slab_storage ? col : d.gidx[(int64_t)s * B + col]) : 0;
+      double cor[LAG_MAX] = {0.0, 0.0, 0.0};
+      for (int l = LAG_MAX - 1; l >= 0; --l) {  // (the older lists are published first)
+        const int sp = s - 1 - l;
+        if (l >= lag || sp < d.seg0) continue;
+        if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + sp + 1, d.sync, 7);
+        __syncthreads();  // (also: the partial sums above are consumed)
+        const int slot = sp % NSLOT;
+        const int nr = ld_sc1_int(d.pend_n + NSLOT + slot);  // real entries (no padding)
+        const int *pgi = d.pend_gi + slot * d.pend_stride;
+        const double *pbo = d.pend_bo + slot * d.pend_stride, *pbn = d.pend_bn + slot * d.pend_stride;
+        for (int e = t; e < nr; e += NT) {
+          s_lg[e] = ld_sc1_int(pgi + e);
+          s_ld[e] = ld_sc1(pbn + e) - ld_sc1(pbo + e);
+        }
+        __syncthreads();
+        const int gp = d.gblk[sp];
+        const double *C = l == 0 ? (gb == (gp + 1) % d.nb ? d.xgram + (int64_t)gp * B * B : d.xgramT + (int64_t)gb * B * B)
+                        : l == 1 ? (gb == (gp + 2) % d.nb ? d.xgram2 + (int64_t)gp * B * B : d.xgram2T + (int64_t)gb * B * B)
+                                 : (gb == (gp + 3) % d.nb ? d.xgram3 + (int64_t)gp * B * B : d.xgram3T + (int64_t)gb * B * B);
+        if (t < RED_NT) {
+          const int e0 = part * nr / np, e1 = (part + 1) * nr / np;
+          double a = 0.0;
+          if (col < bs) {
+            for (int e = e0; e < e1; e += 8) {
+              double v[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) v[u] = e + u < e1 ? C[(int64_t)s_lg[e + u] * B + gic] : 0.0;
+#pragma unroll
+              for (int u = 0; u < 8; ++u)
+                if (e + u < e1) a += v[u] * s_ld[e + u];
+            }
+          }
+          s_red[part * cw + cl] = a;
+        }
+        __syncthreads();
+        if (t < cw) {
+          double c = s_red[t];
+          for (int p = 1; p < np; ++p) c += s_red[p * cw + t];
+          cor[l] = c;
+        }
+      }
+      if (t < cw && col < bs) tot = tot - ((cor[0] + cor[1]) + cor[2]);
+    }
+    if (t < cw) st_sc1(d.slab2 + par * d.slab2_stride + col, tot);
+    publish_add(d.sync + SY_GDONE + 32 * par, 1);
+    if (prof && t == 0) { tr_first(d, s, TR_L2_FIRST); tr_last(d, s, TR_L2_LAST); }
   }
 }
 
@@ -3619,7 +3704,7 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
   if (blockIdx.x == 0) {
     solver_role<HS, B>(d, it, nslot, smem);
   } else if ((int)blockIdx.x > nsg) {
-    reduce_role(d, (int)blockIdx.x - 1 - nsg, nsg, nred, d.sc->prof_on);
+    reduce_role(d, (int)blockIdx.x - 1 - nsg, nsg, nred, d.sc->prof_on, reinterpret_cast<double *>(smem));
   } else {
     // streamer LDS: residual rows, [value tables of four blocks (2-bit codes)], the change list
     // being applied, member indices of two blocks (fused_config)
@@ -3679,7 +3764,7 @@ __global__ __launch_bounds__(NT, 1) void k_sweep_stream(Dev d, int nsg, int rpw,
   __shared__ int s_pf[NT / 64];
   if (!sweep_census(d, nsg + 1 + nred, &s_ok)) return;
   if ((int)blockIdx.x >= nsg) {
-    reduce_role<NT>(d, (int)blockIdx.x - nsg, nsg, nred, d.sc->prof_on);
+    reduce_role<NT>(d, (int)blockIdx.x - nsg, nsg, nred, d.sc->prof_on, reinterpret_cast<double *>(smem));
     return;
   }
   double *eps_l = reinterpret_cast<double *>(smem);
@@ -4115,7 +4200,17 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
   rpw = std::max<int64_t>(SROWS, (rpw + align - 1) / align * align);
   const int nsg = (int)((d.N + rpw - 1) / rpw);
   const int npass = (int)((rpw + SROWS - 1) / SROWS);
-  const int nred = ngr(nsg);
+  // reducers: 4 (BRR_NRED: another power of two, diagnostics), each owning B / nred columns
+  // (reduce_role); the streamers still arrive in groups of FUSED_GROUP.  Same box, sweeps/s for
+  // 1 / 2 / 4 / 8 reducers: C2 2-bit 45.2 / 51.2 / 53.0 / 52.9, C3 10.8 / 10.8 / 10.9 / 10.7, C2 f32
+  // (ms per step, driver's window) 32.77 / 32.40 / 32.46 / 33.05 -- more reducer workgroups slow the
+  // stream (32: C2 34.4 ms); the round-3 form (4 reducers, each a group of 64 streamers for all B
+  // columns, the solver summing 4 rows) 47.5 / 10.35 / 32.64 (profiles/r04g_ab.log)
+  const char *nre = getenv("BRR_NRED");
+  const int nred_cap = nre && atoi(nre) >= 1 ? atoi(nre) : 4;
+  int nred = 1;
+  while (2 * nred <= nred_cap && 1 + nsg + 2 * nred <= cus && d.B % (2 * nred) == 0 && d.B / (2 * nred) >= 8) nred *= 2;
+  if (RED_NT % (d.B / nred) != 0) return false;
   if (nsg > d.RG + 1) return false;  // slab1 rows
   const bool xf = d.Xc != nullptr;
   // BRR_FUSED_SINGLE=1: every role in one k_sweep grid (the PMC passes' form, launch_sweep_fused)
@@ -4183,8 +4278,9 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
   cfg->rpw = (int)rpw;
   cfg->npass = npass;
   cfg->nslot = nslot;
-  cfg->ngroups = nred;
+  cfg->ngroups = 1;  // slab2 rows: every column's whole sum
   cfg->nred = nred;
+  cfg->narr = ngr(nsg);
   cfg->lds = lds;
   cfg->ccache = (xf && ccache) ? 1 : 0;
   cfg->f32cc = (!xf && ccache) ? 1 : 0;

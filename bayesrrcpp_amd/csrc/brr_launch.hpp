@@ -37,7 +37,7 @@ hipError_t launch_slab_total(const Dev &d, int s, hipStream_t st);
 hipError_t launch_group_sum(const GroupPtrs &p, int64_t n, hipStream_t st);
 hipError_t launch_prep(const Dev &d, uint32_t it, hipStream_t st);
 struct FusedCfg {
-  int nsg = 0, rpw = 0, npass = 0, nslot = 0, ngroups = 0, nred = 0;
+  int nsg = 0, rpw = 0, npass = 0, nslot = 0, ngroups = 0, nred = 0, narr = 0;
   int ccache = 0;  // the streamers keep the last blocks' code tiles in LDS (2-bit storage; f32: see f32cc)
   int f32cc = 0;   // f32 storage: room for the class-code cache (used when Dev::xcodes is set: k_sweep_stream<2>)
   int split = 0;   // solver and streaming workgroups as two kernels side by side (else one k_sweep)

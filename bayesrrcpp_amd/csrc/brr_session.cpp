@@ -419,8 +419,17 @@ int do_sweep_local(brr_session *s) {
     d.abase = s->abase;  // residency census epoch of this launch
     s->abase += s->fused.nsg + 1 + s->fused.nred;
     Dev dp = d;
-    dp.NG = s->fused.ngroups;
-    dp.gtarget = s->fused.ngroups;
+    dp.NG = s->fused.ngroups;  // (1: the reducers write every column's whole sum)
+    dp.gtarget = s->fused.nred;
+    dp.ngr = s->fused.narr;
+    // the cross-Gram corrections in the reducers for the BayesR family at B <= 128 (C3 10.42 ->
+    // 10.88 sweeps/s); not for the Horseshoe, whose dense lists put the reducers' gathers on the
+    // solver's critical path (C4 13.06 -> 12.43), nor at B = 512 (sparse lists); BRR_RED_CORR=0|1
+    // overrides (profiles/r04g_ab.log)
+    {
+      const char *rc = getenv("BRR_RED_CORR");
+      dp.rcorr = rc ? (atoi(rc) != 0) : (s->B <= 128 && s->model != MODEL_HORSESHOE);
+    }
     dp.slab_storage = d.Xc != nullptr || d.xcodes != nullptr;  // streamers read blocks in storage order (2-bit, f32 code cache)
     if (s->timing) {
       const size_t i0 = s->ev_used;
@@ -1734,6 +1743,7 @@ int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
     case 106: *out = (double)s->d.lag; return 0;  // pipeline lag
     case 107: *out = (double)s->gram_np_init; return 0;  // Gram kernel: class planes of k_gram_int (0 = FP64 k_gram)
     case 130: *out = (double)s->census_failures; return 0;  // residency census failures so far
+    case 131: *out = (double)s->fused.nred; return 0;       // fused sweep: reducer workgroups (column slices)
     case 109: *out = (double)(s->fused.nsg > 0 ? s->fused.stnt : 0); return 0;  // threads per streaming workgroup
     case 108: *out = (double)(s->fused.nsg > 0 && sc.lag_next >= 2 ? s->d.lag : 1); return 0;  // the next sweep's pipeline lag
     case 110: case 111: case 112: case 113: case 114: case 115: case 116: case 117: case 118: case 119:

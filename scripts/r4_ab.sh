@@ -12,7 +12,7 @@ for rep in $(seq 1 ${REPS:-2}); do
       # name:library[:K=V] (empty library: the in-tree build; K=V: an environment variable for this variant)
       IFS=: read -r vname lib venv <<< "$v"
       if [ -n "$lib" ]; then export BRR_LIB=$lib; else unset BRR_LIB; fi
-      env $venv timeout -k 10 240 python -u bench.py --no-cpu-baseline --no-roofline-events $cargs > gpurun_out/r4ab_${cname}_${vname}_$rep.log 2>&1 \
+      env $(echo "$venv" | tr "," " ") timeout -k 10 240 python -u bench.py --no-cpu-baseline --no-roofline-events $cargs > gpurun_out/r4ab_${cname}_${vname}_$rep.log 2>&1 \
         || { echo "$cname $vname FAILED"; tail -20 gpurun_out/r4ab_${cname}_${vname}_$rep.log; exit 1; }
       python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('$rep $cname $vname', d['value'], d['ms_per_step'])" gpurun_out/r4ab_${cname}_${vname}_$rep.log
     done
