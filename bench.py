@@ -525,7 +525,7 @@ def main():
             launches = max(1, tm["stream_launches"] // nbl)
             bytes_launch = x_bytes
             kname = ("row-shard marker loop (per block: k_stream, k_slab_total, ncclAllReduce of the B dots, k_solve)"
-                     if rows else "k_sweep (fused marker loop: streaming + solver workgroups)")
+                     if rows else "k_sweep_solve + k_sweep_stream (fused marker loop: solver, streaming and reducing workgroups)")
         else:
             launches = max(1, tm["stream_launches"])
             bytes_launch = x_bytes * Bsz / Pl
@@ -543,9 +543,9 @@ def main():
                 "sweep_hbm_gbs": round(x_bytes / (ms * 1e-3) / 1e9, 1),
                 # what limits this configuration in measurement; frac is
                 # always against the HBM roofline of the algorithmic bytes
-                "limiter": ("streaming workgroups' 2-bit decode-dot: instruction latency at 2 waves per SIMD (VALUBusy ~33 %), not HBM" if x2 and model != L.MODEL_GROUPS
+                "limiter": ("solver workgroup's per-block time at lag 1 (dots poll, decisions, write-back drain) and the hand-over latency; the decode-dot is not the bound" if x2 and model not in (L.MODEL_GROUPS, L.MODEL_HORSESHOE)
                             else "solver workgroup's serial chain" if model == L.MODEL_GROUPS
-                            else "HBM: stream + re-read of every changed column (2x bytes)" if model == L.MODEL_HORSESHOE
+                            else "solver's phase A: Gram + cross-Gram blocks (256 KB per block) at one CU's share of HBM, beside a stream that re-reads every column (2x bytes)" if model == L.MODEL_HORSESHOE
                             else "HBM stream")}
     if args.trace_sweeps:
         # per-sweep wall time and changed markers of a fresh chain's first sweeps (diagnostic)
