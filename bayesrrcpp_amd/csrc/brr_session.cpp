@@ -1136,13 +1136,15 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     // order (whole column blocks), but a REFERENCE block holds arbitrary columns -- the per-block
     // kernels read each member column by index
     const bool ref2bit = s->x2bit && s->order_mode == BRR_ORDER_REFERENCE;
-    // BRR_F32_CODE_CACHE=1: f32 storage in BLOCKED order keeps the streamed blocks' class codes in
-    // LDS (used when init finds every column class-coded) and applies the change lists from them
-    // instead of re-reading X.  Opt-in: it removes the apply's HBM re-read but not its time -- C4
-    // 13.42 against 13.87 sweeps/s (profiles/r03cc_c4*.log): the apply is bound by its LDS and
-    // issue work, not by HBM
+    // f32 storage in BLOCKED order: keep the streamed blocks' class codes in LDS (used when init
+    // finds every column class-coded, and where LDS holds lag + 2 blocks of them) and apply the
+    // change lists from them instead of re-reading X -- on by default for the Horseshoe, whose
+    // lists hold every column of a block (C4 13.05 -> 14.1 sweeps/s with the round-4 apply tables
+    // and reducers, profiles/r04i_ab.log; round 3: 13.87 -> 13.42); the other samplers' lists are
+    // short (C2, C3: no change).  BRR_F32_CODE_CACHE=0|1 overrides.
     const char *fcc = getenv("BRR_F32_CODE_CACHE");
-    const bool f32cc = !s->x2bit && s->order_mode == BRR_ORDER_BLOCKED && fcc && fcc[0] == '1';
+    const bool f32cc = !s->x2bit && s->order_mode == BRR_ORDER_BLOCKED &&
+                       (fcc ? fcc[0] == '1' : model == MODEL_HORSESHOE);
     if (rows || ref2bit || (pb && pb[0] == '1') || !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused, f32cc))
       s->fused = FusedCfg{};
     if (s->fused.nsg == 0) d.lag = 1;
