@@ -702,8 +702,10 @@ __host__ __device__ constexpr size_t gram_int_lds(int NP) {
 }
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
+// (NP <= 2, the genotype case: two workgroups per CU -- 8 waves, one's class-plane expansion beside
+// the other's matrix-core products; the register budget of two waves per SIMD)
 template <int NP>
-__global__ __launch_bounds__(256) void k_gram_int(Dev d, const uint8_t *Xk, const int *member, const int *bsz, int B,
+__global__ __launch_bounds__(256, NP <= 2 ? 2 : 1) void k_gram_int(Dev d, const uint8_t *Xk, const int *member, const int *bsz, int B,
                                                   int nb, int shift, double *G, double *GT) {
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   uint8_t *stg = reinterpret_cast<uint8_t *>(gsm);  // the k loop's indicator planes
@@ -998,15 +1000,33 @@ __global__ __launch_bounds__(256) void k_perm_blockorder(Dev d, uint32_t it, int
   for (int64_t s = threadIdx.x; s < nb; s += blockDim.x) d.blkorder[s] = (int)(((rot + dir * s) % nb + nb) % nb);
 }
 
+// The same Fisher-Yates permutation as fisher_yates_dev: the draws do not depend on the swaps, so the
+// workgroup forms them in parallel first (step i uses word i & 3 of Philox counter i >> 2) and one
+// thread then only swaps in LDS (94 -> ~20 µs per sweep at C2: the Philox rounds were on the serial path)
 __global__ void k_perm_within(Dev d, uint32_t it, int identity) {
   __shared__ int w[BMAX];
+  __shared__ uint32_t jr[BMAX];
   const int s = blockIdx.x;
   const int b = d.blkorder[s];
   const int size = (int)min((int64_t)d.B, d.M - (int64_t)b * d.B);
+  const uint32_t ent = (uint32_t)(d.col_offset / d.B + b);
   for (int i = threadIdx.x; i < size; i += blockDim.x) w[i] = i;
+  if (!identity)
+    for (int g = threadIdx.x; 4 * g < size; g += blockDim.x) {
+      const uint4 r = philox(d.seed, (uint32_t)g, T_PERM_WITHIN, ent, it);
+      jr[4 * g] = r.x;
+      if (4 * g + 1 < BMAX) jr[4 * g + 1] = r.y;
+      if (4 * g + 2 < BMAX) jr[4 * g + 2] = r.z;
+      if (4 * g + 3 < BMAX) jr[4 * g + 3] = r.w;
+    }
   __syncthreads();
   if (threadIdx.x == 0 && !identity)
-    fisher_yates_dev(d.seed, w, size, T_PERM_WITHIN, (uint32_t)(d.col_offset / d.B + b), it);
+    for (int i = size - 1; i >= 1; --i) {
+      const int j = (int)(((uint64_t)jr[i] * (uint64_t)(i + 1)) >> 32);
+      const int tmp = w[i];
+      w[i] = w[j];
+      w[j] = tmp;
+    }
   __syncthreads();
   for (int i = threadIdx.x; i < d.B; i += blockDim.x) {
     d.member[(int64_t)s * d.B + i] = i < size ? b * d.B + w[i] : 0;
@@ -2730,14 +2750,8 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     int m = 0;
     if (pos < bs) {
       m = Lm[pos];
-      const int ks = Lks[pos];
       bnv = Lbn[pos];
       bov = Lbo[pos];
-      d.beta[m] = bnv;
-      if (!HS) {
-        if (ks != FALLTHROUGH) d.comp[m] = ks;
-        d.sel[m] = ks != FALLTHROUGH;
-      }
       changed = bnv != bov;
     }
     const uint64_t bal = __ballot(changed);
@@ -2806,6 +2820,22 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       if (tce) atomicAdd(&d.sc->prof[17], (unsigned long long)(tp3 - tce));  // chain end -> all waves past it
       atomicAdd(&d.sc->prof[18], (unsigned long long)nov);                     // rows served by the ring
       atomicAdd(&d.sc->prof[19], (unsigned long long)npred);                   // positions predicted to change
+    }
+  }
+  // the block's state for later sweeps (beta, comp, sel: BayesRv2.cpp:226-245) after the publish: off
+  // the streamers' path (the drain above covers the change list only); these stores retire at the
+  // wave's next vmcnt wait, the next block's phase A, and before the sweep's k_markers
+#pragma unroll
+  for (int c = 0; c < NPT; ++c) {
+    const int pos = t + NT * c;
+    if (pos < bs) {
+      const int m = Lm[pos];
+      d.beta[m] = Lbn[pos];
+      if (!HS) {
+        const int ks = Lks[pos];
+        if (ks != FALLTHROUGH) d.comp[m] = ks;
+        d.sel[m] = ks != FALLTHROUGH;
+      }
     }
   }
 }
