@@ -16,7 +16,7 @@ ORDER_BLOCKED, ORDER_REFERENCE, ORDER_IDENTITY = 0, 1, 2
 X_F32, X_2BIT = 0, 1  # brr_x_storage
 (MU, SIGMAE, SIGMAG, SIGMAF, TAU, ETA, C2, SUMSQ_BETA) = range(8)
 (BETA, COMP, EPS, SIGMAGG, PI, ALPHA, LAMBDA, XSQ, ORDER, VCOUNT, BETAACUM, HSV) = range(12)
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 LOG_FN = C.CFUNCTYPE(None, C.c_char_p, C.c_void_p)
 
@@ -39,7 +39,7 @@ class Options(C.Structure):
 
 # every symbol include/brr.h declares (checked by tests/test_capi.py)
 EXPORTED = [
-    "brr_options_default", "brr_last_error", "brr_device_count",
+    "brr_options_default", "brr_options_effective", "brr_last_error", "brr_device_count", "brr_device_memory",
     "brr_BayesRSamplerV2", "brr_BayesRSamplerV2Groups", "brr_BRV2Grstart", "brr_HorseshoeR",
     "brr_session_create", "brr_session_destroy", "brr_session_upload_x_f64",
     "brr_session_upload_x_f32", "brr_session_upload_bed", "brr_session_synthesize", "brr_session_synth_partial_y",
@@ -74,8 +74,10 @@ def lib():
     L = C.CDLL(path)
     vp = C.c_void_p
     L.brr_options_default.argtypes = [C.POINTER(Options)]
+    L.brr_options_effective.argtypes = [C.POINTER(Options), C.POINTER(Options)]
     L.brr_last_error.restype = C.c_char_p
     L.brr_device_count.restype = C.c_int
+    L.brr_device_memory.argtypes = [C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.brr_BayesRSamplerV2.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, D, C.c_int64,
                                       C.c_int64, D, C.c_double, C.c_double, C.c_double, C.c_double,
                                       C.c_double, D, C.c_int32, C.POINTER(Options)]
@@ -145,6 +147,13 @@ def lib():
     L.brr_session_output_close.argtypes = [vp, C.POINTER(C.c_int32)]
     _lib = L
     return L
+
+
+def device_memory(device=0):
+    """(free, total) bytes of a HIP device."""
+    f, t = C.c_int64(), C.c_int64()
+    check(lib().brr_device_memory(device, C.byref(f), C.byref(t)), "device_memory")
+    return f.value, t.value
 
 
 def last_error() -> str:

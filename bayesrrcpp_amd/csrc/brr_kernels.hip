@@ -163,8 +163,9 @@ __device__ __forceinline__ int ld_sc1_int(const int *p) {
 // that will use it next until its reducer overwrites it with the dot -- a signalling-NaN bit pattern
 // that arithmetic never produces (it yields quiet NaNs), carrying the block's session-wide epoch
 // (Dev::sbase + s) so that a stale value of an earlier block is never mistaken for ready data.
+constexpr unsigned long long SENTINEL_HI = 0x7FF40000ull;  // the high word of every sentinel
 __host__ __device__ inline unsigned long long slab_sentinel(int epoch) {
-  return 0x7FF4000000000000ull | (unsigned long long)(unsigned)epoch;
+  return (SENTINEL_HI << 32) | (unsigned long long)(unsigned)epoch;
 }
 
 // Bounded wait (one lane) for a device counter published by a kernel running concurrently on
@@ -2501,7 +2502,6 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       // the dots are by visit position, or by in-block (storage) index when the 2-bit streamers
       // read the block in storage order (a permutation of 0 .. bs-1; columns bs .. B-1 are unread)
       const int sidx = pos < bs && d.slab_storage ? Lgi[pos] : pos;
-      const unsigned long long sent = slab_sentinel(d.sbase + s);
       for (int g0 = 0; g0 < d.NG; g0 += 16) {
         unsigned long long v[16];
         for (uint32_t n = 0;; ++n) {
@@ -2509,7 +2509,9 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
 #pragma unroll
           for (int u = 0; u < 16; ++u) {
             v[u] = g0 + u < d.NG ? ld_sc1_u64(slab2 + (int64_t)(g0 + u) * B + sidx) : 0ull;
-            ready = ready && (!persistent || v[u] != sent);
+            // any sentinel is "not yet": a stale one of another epoch (a failed launch's slot) waits
+            // into the bounded timeout instead of being summed as data
+            ready = ready && (!persistent || (v[u] >> 32) != (SENTINEL_HI));
           }
           if (ready) break;
           if (n > SPIN_MAX) {  // bounded, as wait_geq: the host reports the protocol error
@@ -3715,12 +3717,16 @@ __device__ BRR_SOLVER_INL void solver_role(const Dev &d, uint32_t it, int nslot,
   }
 }
 
+// XF: 0 f32 storage (with the list prefetch when pfe > 0), 1 2-bit codes, 2 f32 storage with the
+// class-code cache -- the streaming roles of k_sweep_stream<XF> at 512 threads, so that a PMC pass of
+// this form counts the path the two-kernel default times (C2 f32: XF 0 + pfe; C4: XF 2)
 template <bool HS, int B, int XF>
 __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int nslot, int nsg, int rpw, int npass,
-                                                        int nred, int ccache) {
+                                                        int nred, int ccache, int pfe) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_np[2];
   __shared__ int s_ok;
+  __shared__ int s_pf[SWEEP_NW];
   // residency census: every workgroup must be running before any waits on another.  A workgroup whose census
   // timed out -- or that arrives after another one's did -- leaves before touching any state,
   // so a failed census costs one sweep's marker loop, never the chain's consistency.
@@ -3749,9 +3755,11 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
     // (table storage) the apply's value x delta tables, then the code cache
     double *s_w = XF ? s_part + SWEEP_NW * SROWS : nullptr;
     uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_w + (int64_t)(d.B + 16) * 4) : nullptr;
+    // (f32 storage) the list prefetch's staging area: pfe entries x npass passes x 1 KiB
+    float *s_stage = reinterpret_cast<float *>(s_part + SWEEP_NW * SROWS);
     stream_role<STREAM_CW, XF == 1 ? STREAM_P2 : STREAM_P, XF>(d, (int)blockIdx.x - 1, rpw, npass, eps_l, s_pidx, s_pbo,
-                                                         s_pbn, s_np, s_lut, s_mem, s_part, s_codes, 0, nullptr, nullptr,
-                                                         s_w);
+                                                         s_pbn, s_np, s_lut, s_mem, s_part, s_codes, XF ? 0 : pfe, s_pf,
+                                                         s_stage, s_w);
   }
 }
 
@@ -4169,16 +4177,17 @@ hipError_t launch_stream(const Dev &d, int s, const double *eps_in, double *eps_
 // configuration cannot be made resident (the per-block kernels are used then).
 // (B = 64 never fuses: a block must give every wave whole STREAM_CW-column chunks)
 template <bool HS, int B>
-static const void *sweep_fn(bool xf) {
-  return xf ? (const void *)k_sweep<HS, B, 1> : (const void *)k_sweep<HS, B, 0>;
+static const void *sweep_fn(int xv) {
+  return xv == 1 ? (const void *)k_sweep<HS, B, 1> : xv == 2 ? (const void *)k_sweep<HS, B, 2> : (const void *)k_sweep<HS, B, 0>;
 }
 
-static const void *sweep_kernel(int model, int B, bool xf) {
+// xv: the streaming variant (stream_variant)
+static const void *sweep_kernel(int model, int B, int xv) {
   const bool hs = model == MODEL_HORSESHOE;
   switch (B) {
-    case 128: return hs ? sweep_fn<true, 128>(xf) : sweep_fn<false, 128>(xf);
-    case 256: return hs ? sweep_fn<true, 256>(xf) : sweep_fn<false, 256>(xf);
-    case 512: return hs ? sweep_fn<true, 512>(xf) : sweep_fn<false, 512>(xf);
+    case 128: return hs ? sweep_fn<true, 128>(xv) : sweep_fn<false, 128>(xv);
+    case 256: return hs ? sweep_fn<true, 256>(xv) : sweep_fn<false, 256>(xv);
+    case 512: return hs ? sweep_fn<true, 512>(xv) : sweep_fn<false, 512>(xv);
     default: return nullptr;
   }
 }
@@ -4250,7 +4259,7 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
   // still a whole number of 16-column chunks); BRR_STREAM_NT=512 keeps eight waves (diagnostics)
   const char *snt_env = getenv("BRR_STREAM_NT");
   const int stnt = (split && xf && d.B % (16 * STREAM_CW) == 0 && !(snt_env && atoi(snt_env) == 512)) ? 1024 : SWEEP_NT;
-  const void *fn = split ? solve_kernel(d.model, d.B) : sweep_kernel(d.model, d.B, xf);
+  const void *fn = split ? solve_kernel(d.model, d.B) : sweep_kernel(d.model, d.B, xf ? 1 : 0);
   const void *fst = split ? stream_kernel(xf ? 1 : 0, stnt) : nullptr;
   if (!fn) return false;
   hipFuncAttributes attr, attr_st;
@@ -4266,7 +4275,7 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
   // streamers: residual rows, [the value tables of two blocks], the change list (indices, old and
   // new betas), the member indices of two blocks in LDS
   // (f32 storage with a class-code cache: the value tables and code tiles as for 2-bit storage)
-  const bool tables = xf || (f32cc && split);
+  const bool tables = xf || f32cc;
   const size_t lut_bytes = (size_t)d.B * 32 * (d.lag + 3) + (size_t)(d.B + 16) * 32;  // + the apply's x delta tables
   const size_t eps_base = (size_t)npass * SROWS * sizeof(double) + (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int)) +
                           2 * sizeof(int) * d.B + (size_t)SWEEP_NW * SROWS * sizeof(double);
@@ -4276,14 +4285,20 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
   const size_t st_lds = eps_base + (xf || ccache ? lut_bytes : 0) + (ccache ? code_bytes : 0);
   // (split, f32 storage) the list prefetch's staging area in the room left: up to 32 entries of
   // npass KiB, when every wave has at most one pass (BRR_LIST_PREFETCH=0: off)
+  // (one-kernel form: the same staging area where the grid's LDS request leaves room, so that the PMC
+  // passes count the prefetching stream)
   int pfe = 0;
-  if (split && !xf && npass <= SWEEP_NW && !(getenv("BRR_LIST_PREFETCH") && getenv("BRR_LIST_PREFETCH")[0] == '0')) {
-    const size_t room = st_budget > st_lds ? st_budget - st_lds : 0;
+  if (!xf && !ccache && npass <= SWEEP_NW && !(getenv("BRR_LIST_PREFETCH") && getenv("BRR_LIST_PREFETCH")[0] == '0')) {
+    const size_t cap_lds = split ? st_budget : budget;
+    const size_t room = cap_lds > st_lds ? cap_lds - st_lds : 0;
     pfe = (int)std::min<size_t>(32, room / ((size_t)npass * SROWS * sizeof(float))) / 16 * 16;
   }
   const size_t st_lds_pf = st_lds + (size_t)pfe * npass * SROWS * sizeof(float);
-  const size_t lds = split ? fixed + (size_t)nslot * 8 * d.B : std::max(fixed + (size_t)nslot * 8 * d.B, st_lds);
+  const size_t lds = split ? fixed + (size_t)nslot * 8 * d.B : std::max(fixed + (size_t)nslot * 8 * d.B, st_lds_pf);
   if (lds > budget || st_lds > st_budget) return false;
+  // (one-kernel form) the variant this configuration launches (launch_sweep_fused)
+  const int xv1 = xf ? 1 : ccache ? 2 : 0;
+  if (!split) fn = sweep_kernel(d.model, d.B, xv1);
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) != hipSuccess) return false;
   if (split && hipFuncSetAttribute(fst, hipFuncAttributeMaxDynamicSharedMemorySize, (int)st_budget) != hipSuccess)
     return false;
@@ -4349,9 +4364,13 @@ hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipS
     if (e == hipSuccess) e = hipStreamWaitEvent(st, ev_done, 0);
     return e;
   }
-  const void *fn = sweep_kernel(d.model, d.B, d.Xc != nullptr);
+  // one kernel: the same streaming variant and list prefetch as the two-kernel form (at 512 threads)
+  const int xv = stream_variant(d, c);
+  const void *fn = sweep_kernel(d.model, d.B, xv);
   if (!fn) return hipErrorInvalidValue;
-  void *args[] = {&dd, &it, &nslot, &nsg, &rpw, &npass, &nred, &cc};
+  if (xv == 2) cc = 1;
+  int pfe = xv == 0 ? c.pfe : 0;
+  void *args[] = {&dd, &it, &nslot, &nsg, &rpw, &npass, &nred, &cc, &pfe};
   return hipLaunchKernel(fn, dim3((unsigned)(c.nsg + 1 + c.nred)), dim3(SWEEP_NT), args, (unsigned)c.lds, st);
 }
 

@@ -24,6 +24,8 @@
 #include <thread>
 #include <vector>
 
+#include <unistd.h>
+
 #include "../../include/brr.h"
 #include "brr_sample.hpp"
 
@@ -59,6 +61,14 @@ class CsvWriter {
     }
     cv_.notify_one();
     if (th_.joinable()) th_.join();  // drain everything queued (the reference may drop rows)
+  }
+  // after close(): cut the file back to the headers and the first n sample rows (a failed chain keeps
+  // only the rows of states a device check confirmed)
+  void truncate_rows(int64_t n) {
+    const int64_t off = n <= 0 ? hdr_end_ : row_end_[(size_t)std::min<int64_t>(n, (int64_t)row_end_.size()) - 1];
+    fflush(f_);
+    if (ftruncate(fileno(f_), (off_t)off) != 0) err_ = -3;
+    fseek(f_, 0, SEEK_END);
   }
 
  private:
@@ -112,14 +122,21 @@ class CsvWriter {
         it = std::move(q_.front());
         q_.pop_front();
       }
-      if (it.is_header) { fputs(it.h.c_str(), f_); continue; }
+      if (it.is_header) {
+        fputs(it.h.c_str(), f_);
+        pos_ += (int64_t)it.h.size();
+        hdr_end_ = pos_;
+        continue;
+      }
       brr::SampleView v;
       if (brr::sample_ring_wait(s_, it.slot, &v) != 0) {
         err_ = -2;
       } else {
         format(v, it.iteration);
         fwrite(buf_.data(), 1, buf_.size(), f_);
+        pos_ += (int64_t)buf_.size();
       }
+      row_end_.push_back(pos_);  // (a failed row leaves the offset unchanged)
       brr::sample_ring_release(s_, it.slot);
     }
   }
@@ -131,6 +148,8 @@ class CsvWriter {
   char num_[40];
   bool first_ = true;
   int err_ = 0;
+  int64_t pos_ = 0, hdr_end_ = 0;  // bytes written; end of the headers
+  std::vector<int64_t> row_end_;   // file offset after each sample row, in order
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<Item> q_;
@@ -215,8 +234,6 @@ struct Timeline {
     last = t;
   }
 };
-thread_local Timeline *g_tl = nullptr;  // the current one-shot call's timeline (run_chain reports into it)
-
 struct Run {
   int model;
   const char *out;
@@ -226,6 +243,7 @@ struct Run {
   int64_t F;
   Log log;
   bool verbose;
+  Timeline *tl;  // the call's timeline (run_chain reports its per-100-iteration lines into it)
 };
 
 int fail(brr_session *s, const Log &log, int rc) {
@@ -239,7 +257,11 @@ int fail(brr_session *s, const Log &log, int rc) {
 // through the session's sample ring: a device snapshot, an asynchronous copy to pinned memory
 // and the writer thread, so the sampler never waits for a row's D2H copy or its formatting
 // unless the writer is BRR_SAMPLE_RING (default 4) rows behind.
-int run_chain(brr_session *s, const Run &r, CsvWriter *w) {
+// *n_ok: the sample rows pushed up to the last device check that passed (on a failure the caller
+// keeps only those rows in the file)
+int run_chain(brr_session *s, const Run &r, CsvWriter *w, int64_t *n_ok) {
+  *n_ok = 0;
+  int64_t n_rows = 0;
   const char *rd = getenv("BRR_SAMPLE_RING");
   if (int rc = brr::sample_ring_open(s, rd ? atoi(rd) : 4)) return rc;
   w->bind(s, r.model, r.N, r.M, r.G, r.F);
@@ -263,21 +285,24 @@ int run_chain(brr_session *s, const Run &r, CsvWriter *w) {
     const auto ta = std::chrono::steady_clock::now();
     // the device error check (stream sync + read-back) every 16 iterations and at the end: a per-sweep
     // sync left the device idle for the host's launches of every sweep (C1: 7.4 against 6.9 ms)
-    if (int rc = brr::session_sweep(s, 1, (it & 15) == 15 || it + 1 == r.max_it)) return rc;
+    const bool check = (it & 15) == 15 || it + 1 == r.max_it;
+    if (int rc = brr::session_sweep(s, 1, check)) return rc;
     const auto tb = std::chrono::steady_clock::now();
     t_sweep += std::chrono::duration<double, std::milli>(tb - ta).count();
     if (it >= r.burn_in && it % r.thin == 0) {
       int slot = -1;
       if (int rc = brr::sample_ring_push(s, &slot)) return rc;
       w->sample(slot, it);
+      ++n_rows;
       t_push += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count();
       ++n_push;
     }
-    if (g_tl && g_tl->on && ((it + 1) % 100 == 0 || it + 1 == r.max_it)) {
+    if (check) *n_ok = n_rows;  // this sweep's state (and its row) passed the device check
+    if (r.tl && r.tl->on && ((it + 1) % 100 == 0 || it + 1 == r.max_it)) {
       char b[200];
       snprintf(b, sizeof b, "timeline chain it %d: sweeps %.2f ms, %d sample pushes %.2f ms\n", it + 1, t_sweep,
                n_push, t_push);
-      g_tl->log(b);
+      r.tl->log(b);
       t_sweep = t_push = 0;
       n_push = 0;
     }
@@ -302,7 +327,6 @@ int brr_BayesRSamplerV2(const char *outputFile, int seed, int max_iterations, in
   brr_options opt = opts_or_default(opt_in);
   Log log{opt.log, opt.log_userdata};
   Timeline tl(log);
-  g_tl = &tl;
   FILE *f = fopen(outputFile, "w");  // BayesRv2.cpp:69
   if (!f) { log(std::string("brr: cannot open ") + outputFile + "\n"); return -3; }
   CsvWriter w(f);
@@ -324,13 +348,14 @@ int brr_BayesRSamplerV2(const char *outputFile, int seed, int max_iterations, in
   tl.mark("set");
   if (!rc) rc = brr_session_init(s, seed);
   tl.mark("init");
-  Run r{BRR_MODEL_V2, outputFile, max_iterations, burn_in, thinning, N, M, 1, 0, log, opt.verbose != 0};
-  if (!rc) rc = run_chain(s, r, &w);
+  Run r{BRR_MODEL_V2, outputFile, max_iterations, burn_in, thinning, N, M, 1, 0, log, opt.verbose != 0, &tl};
+  int64_t n_ok = 0;
+  if (!rc) rc = run_chain(s, r, &w, &n_ok);
   tl.mark("chain");
   w.close();
+  if (rc) w.truncate_rows(n_ok);  // only rows of device-checked states stay
   fclose(f);
   tl.mark("drain");
-  g_tl = nullptr;
   if (!rc && w.error()) rc = w.error();
   if (rc) return fail(s, log, rc);
   brr_session_destroy(s);
@@ -363,9 +388,11 @@ int brr_BayesRSamplerV2Groups(const char *outputFile, int seed, int max_iteratio
   if (!rc) rc = brr_session_set_fixed(s, fixed);
   if (!rc) rc = brr_session_set_bayesr(s, sigma0, v0E, s02E, v0G, s02G, cva, gAssign);
   if (!rc) rc = brr_session_init(s, seed);
-  Run r{BRR_MODEL_GROUPS, outputFile, max_iterations, burn_in, thinning, N, M, groups, F, log, opt.verbose != 0};
-  if (!rc) rc = run_chain(s, r, &w);
+  Run r{BRR_MODEL_GROUPS, outputFile, max_iterations, burn_in, thinning, N, M, groups, F, log, opt.verbose != 0, nullptr};
+  int64_t n_ok = 0;
+  if (!rc) rc = run_chain(s, r, &w, &n_ok);
   w.close();
+  if (rc) w.truncate_rows(n_ok);  // only rows of device-checked states stay
   fclose(f);
   if (!rc && w.error()) rc = w.error();
   if (rc) return fail(s, log, rc);
@@ -396,9 +423,11 @@ int brr_BRV2Grstart(const char *outputFile, int seed, int max_iterations, int bu
   if (!rc) rc = brr_session_set_bayesr(s, sigma0, v0E, s02E, v0G, s02G, cva, gAssign);
   if (!rc) rc = brr_session_set_restart(s, mu, beta, sigmaE, sigmaGG, epsilon, components);
   if (!rc) rc = brr_session_init(s, seed);
-  Run r{BRR_MODEL_RESTART, outputFile, max_iterations, burn_in, thinning, N, M, groups, 0, log, opt.verbose != 0};
-  if (!rc) rc = run_chain(s, r, &w);
+  Run r{BRR_MODEL_RESTART, outputFile, max_iterations, burn_in, thinning, N, M, groups, 0, log, opt.verbose != 0, nullptr};
+  int64_t n_ok = 0;
+  if (!rc) rc = run_chain(s, r, &w, &n_ok);
   w.close();
+  if (rc) w.truncate_rows(n_ok);  // only rows of device-checked states stay
   fclose(f);
   if (!rc && w.error()) rc = w.error();
   if (rc) return fail(s, log, rc);
@@ -434,9 +463,11 @@ int brr_HorseshoeR(const char *outputFile, int seed, int max_iterations, int bur
     snprintf(b, sizeof b, "initial eta %g\ninitial tau %g\n", eta, tau);
     log(b);
   }
-  Run r{BRR_MODEL_HORSESHOE, outputFile, max_iterations, burn_in, thinning, N, M, 1, 0, log, opt.verbose != 0};
-  if (!rc) rc = run_chain(s, r, &w);
+  Run r{BRR_MODEL_HORSESHOE, outputFile, max_iterations, burn_in, thinning, N, M, 1, 0, log, opt.verbose != 0, nullptr};
+  int64_t n_ok = 0;
+  if (!rc) rc = run_chain(s, r, &w, &n_ok);
   w.close();
+  if (rc) w.truncate_rows(n_ok);  // only rows of device-checked states stay
   fclose(f);
   if (!rc && w.error()) rc = w.error();
   if (rc) return fail(s, log, rc);

@@ -161,9 +161,19 @@ struct brr_session {
   bool ex_owned = false;
   std::vector<double> synth_y;  // this shard's X_causal beta_causal (synthetic cohort)
   ncclComm_t comm = nullptr;
-  // reference visit order state
+  // reference visit order state (owned by the shuffle-ahead thread once it runs, RefAhead)
   GlibcRand grand;
   std::vector<int32_t> ref_order, ref_forder;
+  // REFERENCE order: the next sweep's permutation is shuffled on a host thread while the device runs
+  // the current sweep (the glibc stream does not depend on the chain); the sweep takes it
+  struct RefAhead {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool want = false, have = false, stop = false;
+    std::vector<int32_t> visit, forder;  // the next sweep's: this shard's visit order, fixedI
+  } ahead;
+  std::vector<int32_t> cur_visit, cur_forder;  // the current sweep's (alive while its copies are in flight)
   int32_t *ref_pin[2] = {nullptr, nullptr};  // pinned member buffers of upload_order
   hipEvent_t ref_ev[2] = {nullptr, nullptr};
   int ref_k = 0;
@@ -181,13 +191,24 @@ struct brr_session {
   std::vector<void *> allocs;
   SampleRing ring;
 
+  bool alloc_failed = false;  // after one failed allocation the rest are not attempted
   template <class T>
   int alloc(T **p, int64_t n) {
+    if (alloc_failed) { *p = nullptr; return -2; }
     int rc = dalloc(p, n);
     if (rc == 0) allocs.push_back((void *)*p);
+    else alloc_failed = true;
     return rc;
   }
   ~brr_session() {
+    if (ahead.th.joinable()) {
+      {
+        std::lock_guard<std::mutex> lk(ahead.mu);
+        ahead.stop = true;
+      }
+      ahead.cv.notify_all();
+      ahead.th.join();
+    }
     // nothing may still run on either stream when its buffers go (e.g. a streaming kernel left in
     // flight by a bounded solver timeout): both drain before any hipFree / hipEventDestroy
     if (st_side) (void)hipStreamSynchronize(st_side);
@@ -252,6 +273,49 @@ std::vector<int32_t> shard_visit(const brr_session *s) {
   for (const int32_t m : s->ref_order)
     if (m >= s->col_offset && m < s->col_offset + s->M) v.push_back((int32_t)(m - s->col_offset));
   return v;
+}
+
+// The shuffle-ahead thread: one sweep's permutations per request, in the reference's order of draws
+// (fixedI before markerI, BayesRv2Groups.cpp:216,227; markerI, BayesRv2.cpp:182), so the glibc stream is
+// consumed exactly as a synchronous shuffle would.
+void ref_ahead_run(brr_session *s) {
+  auto &a = s->ahead;
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> lk(a.mu);
+      a.cv.wait(lk, [&] { return a.want || a.stop; });
+      if (a.stop) return;
+    }
+    if (s->F > 0) s->grand.shuffle(s->ref_forder);
+    s->grand.shuffle(s->ref_order);
+    std::vector<int32_t> v = shard_visit(s), f = s->ref_forder;
+    {
+      std::lock_guard<std::mutex> lk(a.mu);
+      a.visit.swap(v);
+      a.forder.swap(f);
+      a.want = false;
+      a.have = true;
+    }
+    a.cv.notify_all();
+  }
+}
+
+// this sweep's REFERENCE permutations (into s->cur_visit / cur_forder), and the next sweep's shuffle
+// started on the thread
+void ref_take(brr_session *s) {
+  auto &a = s->ahead;
+  std::unique_lock<std::mutex> lk(a.mu);
+  if (!a.th.joinable()) {
+    a.want = true;
+    a.th = std::thread(ref_ahead_run, s);
+  }
+  a.cv.wait(lk, [&] { return a.have; });
+  s->cur_visit.swap(a.visit);
+  s->cur_forder.swap(a.forder);
+  a.have = false;
+  a.want = true;  // the next sweep's, while this one runs on the device
+  lk.unlock();
+  a.cv.notify_all();
 }
 
 int upload_order(brr_session *s, const std::vector<int32_t> &order) {
@@ -379,12 +443,10 @@ int do_sweep_local(brr_session *s) {
     if (s->order_mode == BRR_ORDER_BLOCKED) {
       HIPCHK(launch_perm(d, it, s->shard, false, s->st));
     } else if (s->order_mode == BRR_ORDER_REFERENCE) {
-      if (s->F > 0) {  // fixedI shuffled before markerI (BayesRv2Groups.cpp:216,227)
-        s->grand.shuffle(s->ref_forder);
-        HIPCHK(hipMemcpyAsync(d.forder, s->ref_forder.data(), (size_t)s->F * 4, hipMemcpyHostToDevice, s->st));
-      }
-      s->grand.shuffle(s->ref_order);
-      if (int rc = upload_order(s, shard_visit(s))) return rc;
+      ref_take(s);  // fixedI and markerI of this sweep, shuffled ahead on the host thread
+      if (s->F > 0)
+        HIPCHK(hipMemcpyAsync(d.forder, s->cur_forder.data(), (size_t)s->F * 4, hipMemcpyHostToDevice, s->st));
+      if (int rc = upload_order(s, s->cur_visit)) return rc;
       if (int rc = encode_layout(s)) return rc;
       HIPCHK(launch_gram(d, 0, d.gram, nullptr, s->st));
       HIPCHK(launch_gram(d, 1, d.xgram, d.xgramT, s->st));
@@ -723,8 +785,11 @@ int coll_init(Coll &c, int32_t seed) {
         }
         HIPCHK(hipMemsetAsync(d.sel, 0, s->M, s->st));
         HIPCHK(hipMemsetAsync(d.alpha, 0, sizeof(double) * std::max(s->F, 1), s->st));
-        if (s->F > 0)  // identity fixed-effect order (IDENTITY mode; REFERENCE overwrites per sweep)
-          if (int rc = h2d(s, d.forder, s->ref_forder.data(), s->F)) return rc;
+        if (s->F > 0) {  // identity fixed-effect order (IDENTITY mode; REFERENCE overwrites per sweep)
+          std::vector<int32_t> idf((size_t)s->F);
+          for (int i = 0; i < s->F; ++i) idf[(size_t)i] = i;
+          if (int rc = h2d(s, d.forder, idf.data(), s->F)) return rc;
+        }
         if (s->model == MODEL_HORSESHOE) {
           std::vector<double> ones((size_t)s->M, 1.0);
           if (int rc = h2d(s, d.lambda, ones.data(), s->M)) return rc;
@@ -783,12 +848,10 @@ int coll_sweep_rows(Coll &c) {
         if (s->order_mode == BRR_ORDER_BLOCKED) {
           HIPCHK(launch_perm(d, it, 0, false, s->st));
         } else if (s->order_mode == BRR_ORDER_REFERENCE) {
-          if (s->F > 0) {  // fixedI shuffled before markerI (BayesRv2Groups.cpp:216,227)
-            s->grand.shuffle(s->ref_forder);
-            HIPCHK(hipMemcpyAsync(d.forder, s->ref_forder.data(), (size_t)s->F * 4, hipMemcpyHostToDevice, s->st));
-          }
-          s->grand.shuffle(s->ref_order);
-          if (int rc = upload_order(s, s->ref_order)) return rc;
+          ref_take(s);  // (a row shard holds every marker: its visit order is the whole permutation)
+          if (s->F > 0)
+            HIPCHK(hipMemcpyAsync(d.forder, s->cur_forder.data(), (size_t)s->F * 4, hipMemcpyHostToDevice, s->st));
+          if (int rc = upload_order(s, s->cur_visit)) return rc;
         } else {
           HIPCHK(launch_perm(d, it, 0, true, s->st));
         }
@@ -895,7 +958,11 @@ void brr_options_default(brr_options *o) {
   o->order_mode = BRR_ORDER_BLOCKED;
   o->shard_count = 1;
   o->row_shard_count = 1;
-  o->exchanges_per_sweep = 0;  // automatic (column shards: the shard count)
+  o->exchanges_per_sweep = 0;  // automatic (column shards: E = 8, capped at the blocks per shard)
+}
+
+void brr_options_effective(const brr_options *in, brr_options *out) {
+  if (out) *out = brr::options_from_caller(in);
 }
 
 const char *brr_last_error(void) { return g_last_error.c_str(); }
@@ -904,6 +971,18 @@ int brr_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+}
+
+int brr_device_memory(int32_t device, int64_t *free_bytes, int64_t *total_bytes) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n < 1) { set_error("no HIP device available"); return -1; }
+  if (device < 0 || device >= n) { set_error("device %d not present", device); return -1; }
+  HIPCHK(hipSetDevice(device));
+  size_t f = 0, t = 0;
+  HIPCHK(hipMemGetInfo(&f, &t));
+  if (free_bytes) *free_bytes = (int64_t)f;
+  if (total_bytes) *total_bytes = (int64_t)t;
+  return 0;
 }
 
 brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_total,
@@ -1020,6 +1099,26 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
   // genotype storage: f32 (default) or 2-bit codes + per-column value tables
   s->x2bit = opt.x_storage == BRR_X_2BIT;
   d.ldc = d.ld / 4;
+  // Preflight: the big buffers against the device's free memory, before any of them is allocated.
+  // A create that cannot fit (e.g. a 200 GB X while an earlier session still holds 250 GB) fails
+  // here with its sizes in the message; BRR_NO_MEM_PREFLIGHT=1 skips it (tests: the allocation
+  // failure path itself).
+  if (!(getenv("BRR_NO_MEM_PREFLIGHT") && getenv("BRR_NO_MEM_PREFLIGHT")[0] == '1')) {
+    size_t mfree = 0, mtotal = 0;
+    if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess) {
+      const double xb = s->x2bit ? (double)d.ldc * s->nb * B + 16.0 * M : 4.0 * (double)d.ld * M;
+      const double grams = 3.0 * 8.0 * (double)s->nb * B * B;  // gram, xgram, xgramT (lag 2 adds two more later)
+      const double small = 8.0 * (double)d.ld * 3 + 8.0 * (double)s->nb * B * (3 + 2 * K) + 64.0 * M + 8.0 * N * std::max<int64_t>(F, 1);
+      const double need = xb + grams + small;
+      if (need > (double)mfree) {
+        set_error("device %d has %.2f GB free of %.2f GB: this session needs %.2f GB (X %.2f GB, Gram blocks %.2f GB, "
+                  "the rest %.2f GB)",
+                  s->device, mfree / 1e9, mtotal / 1e9, need / 1e9, xb / 1e9, grams / 1e9, small / 1e9);
+        delete s;
+        return nullptr;
+      }
+    }
+  }
   if (s->x2bit) {
     rc |= s->alloc(const_cast<uint8_t **>(&d.Xc), d.ldc * s->nb * B);  // whole tiles of the last block
     rc |= s->alloc(const_cast<float **>(&d.xlut), 4 * M);
@@ -1592,10 +1691,19 @@ int brr::session_sweep(brr_session *s, int n, bool check) {
   HIPCHK(hipSetDevice(s->device));
   if (s->nshard > 1 && !s->comm)
     if (int rc = brr_session_exchange_buffers(s, nullptr, nullptr)) return rc;
+  // BRR_SEGMENT_CHECK=0: no device check between exchange segments (measurement of its cost)
+  static const bool seg_check = !(getenv("BRR_SEGMENT_CHECK") && getenv("BRR_SEGMENT_CHECK")[0] == '0');
+  int seg_rc = 0;
   for (int r = 0; r < n; ++r) {
     for (int e = 0; e < s->nex; ++e) {
       const bool last = s->seg == s->nex - 1;
       if (int rc = do_sweep_local(s)) return rc;
+      // an exchange segment before the sweep's last: the device check, as sweep_local's callers get it
+      // (a failed census moves the sweep's later segments onto the per-block kernels instead of fused
+      // launches whose census could no longer pass).  The error is returned after the loop: every rank
+      // still takes part in every collective of the sweep.
+      if (seg_check && s->nex > 1 && s->fused.nsg > 0 && !last)
+        if (int rc = check_device_error(s, true)) seg_rc = rc;
       if (s->nshard > 1 && s->comm) {
         // the exchange step of the column-sharded sweep (E per sweep): the sum of the
         // residual deltas (N doubles) and, after the sweep's last segment only, of the marker
@@ -1616,7 +1724,9 @@ int brr::session_sweep(brr_session *s, int n, bool check) {
       if (int rc = do_sweep_finish(s)) return rc;
     }
   }
-  return check ? check_device_error(s) : 0;
+  if (check)
+    if (int rc = check_device_error(s)) return rc;
+  return seg_rc;
 }
 
 extern "C" {
@@ -1992,9 +2102,12 @@ brr_options options_from_caller(const brr_options *in) {
   brr_options o;
   brr_options_default(&o);
   if (in) {
+    // ABI 4 gave exchanges_per_sweep = 0 its automatic meaning (E = 8); an older caller -- ABI 3 with
+    // the field zeroed, ABI 1 / 2 without it -- keeps the one exchange per sweep its header documented
     if (in->abi_version >= 3) o = *in;
     else if (in->abi_version == 2) std::memcpy(&o, in, offsetof(brr_options, exchanges_per_sweep));
     else std::memcpy(&o, in, offsetof(brr_options, row_shard_rank));
+    if (in->abi_version < 4 && (in->abi_version < 3 || o.exchanges_per_sweep == 0)) o.exchanges_per_sweep = 1;
     o.abi_version = BRR_ABI_VERSION;
   }
   if (o.exchanges_per_sweep < 0) o.exchanges_per_sweep = 0;

@@ -264,6 +264,13 @@ class Session:
             L.lib().brr_session_destroy(self.h)
             self.h = None
 
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()  # device memory goes now, not when a failed test's traceback lets go of the object
+        return False
+
     def __del__(self):
         try:
             self.close()

@@ -130,7 +130,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-markers", type=int, default=3000,
                     help="markers in the bounded CPU-baseline sample (N as in the config)")
-    ap.add_argument("--cpu-sweeps", type=int, default=3)
+    ap.add_argument("--cpu-sweeps", type=int, default=2, help="sweeps per timed repeat of the CPU sample")
+    ap.add_argument("--cpu-repeats", type=int, default=3, help="timed repeats of the CPU sample (median reported)")
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-roofline-events", action="store_true")
     ap.add_argument("--exchanges", type=int, default=0,
@@ -166,7 +167,8 @@ def cpu_baseline_child(args):
     """Runs in a subprocess pinned to ONE core: the reference-faithful CPU oracle (f64, y~
     materialised, single thread -- the reference's package build is single-threaded,
     SURVEY fact 5) on a bounded sample of the same workload."""
-    os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
+    core = sorted(os.sched_getaffinity(0))[0]
+    os.sched_setaffinity(0, {core})
     from oracle import oracle as O
     O.build()
     cfg = CONFIGS[args.config]
@@ -191,10 +193,22 @@ def cpu_baseline_child(args):
         kw.update(cva=CVA)
     o = O.Oracle(model, X, Y, seed=args.seed, order_mode=O.ORDER_REFERENCE, **kw)
     o.sweep(1)  # warm
-    t0 = time.perf_counter()
-    o.sweep(args.cpu_sweeps)
-    dt = time.perf_counter() - t0
-    print(json.dumps({"t_sweep_sample_s": dt / args.cpu_sweeps, "markers": Pm, "N": N}))
+    load0 = _loadavg()
+    runs = []
+    for _ in range(max(1, args.cpu_repeats)):  # repeats: the host's load moves a single run by up to 2x
+        t0 = time.perf_counter()
+        o.sweep(args.cpu_sweeps)
+        runs.append((time.perf_counter() - t0) / args.cpu_sweeps)
+    print(json.dumps({"t_sweep_runs_s": runs, "markers": Pm, "N": N, "core": core,
+                      "loadavg_before": load0, "loadavg_after": _loadavg()}))
+
+
+def _loadavg():
+    try:
+        with open("/proc/loadavg") as f:
+            return " ".join(f.read().split()[:3])
+    except OSError:
+        return None
 
 
 def pmc_traffic(args, N, P, B, fused, x_bytes):
@@ -229,6 +243,7 @@ def host_cpu_model() -> str:
 def cpu_baseline(args, P_full):
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--config", args.config,
            "--cpu-markers", str(args.cpu_markers), "--cpu-sweeps", str(args.cpu_sweeps),
+           "--cpu-repeats", str(args.cpu_repeats),
            "--data-seed", str(args.data_seed)]
     if args.N:
         cmd += ["--N", str(args.N)]
@@ -237,17 +252,23 @@ def cpu_baseline(args, P_full):
         return {"value": None, "unit": "sweeps/s", "cores": 1, "kind": "port",
                 "sample": f"failed: {out.stderr[-300:]}"}
     r = json.loads(out.stdout.strip().splitlines()[-1])
-    t_marker = r["t_sweep_sample_s"] / r["markers"]
+    tm = sorted(t / r["markers"] for t in r["t_sweep_runs_s"])
+    t_marker = tm[len(tm) // 2]  # median of the repeats
     return {
         "value": 1.0 / (t_marker * P_full),
-        "unit": "sweeps/s (extrapolated: 1 / (P x t_marker))",
+        "unit": "sweeps/s (extrapolated: 1 / (P x median t_marker))",
         "cores": 1,
         "kind": "port",
         "host_cpu": host_cpu_model(), "host_nproc": os.cpu_count(),
         "sample": (f"CPU oracle (reference-faithful C restatement, f64, y~ materialised, 1 thread "
-                   f"pinned) N={r['N']} x {r['markers']} markers, {args.cpu_sweeps} sweeps; "
-                   f"t_marker={t_marker * 1e3:.4f} ms; P={P_full}"),
+                   f"pinned to core {r['core']}) N={r['N']} x {r['markers']} markers, {len(tm)} repeats of "
+                   f"{args.cpu_sweeps} sweeps; median t_marker={t_marker * 1e3:.4f} ms; P={P_full}"),
         "t_marker_ms": t_marker * 1e3,
+        "t_marker_min_ms": tm[0] * 1e3,
+        "t_marker_runs_ms": [round(t * 1e3, 4) for t in tm],
+        "value_at_min": 1.0 / (tm[0] * P_full),
+        "pinned_core": r["core"],
+        "host_loadavg": [r["loadavg_before"], r["loadavg_after"]],
     }
 
 

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define BRR_ABI_VERSION 3
+#define BRR_ABI_VERSION 4
 
 enum brr_model { BRR_MODEL_V2 = 0, BRR_MODEL_GROUPS = 1, BRR_MODEL_RESTART = 2, BRR_MODEL_HORSESHOE = 3 };
 
@@ -89,13 +89,23 @@ typedef struct brr_options {
    * less than 1/8 of a sweep's changes of the others late, and the 8-shard chain matches the 1-shard
    * chain within Monte-Carlo error.  1 = north_star's single exchange per sweep (measurably biased
    * from 2 shards on).  Every shard must use the same E.
-   * Ignored without column shards. */
+   * Ignored without column shards.
+   * PROTOCOL BREAK at ABI 4: 0 means automatic (E = 8) only for abi_version >= 4.  A caller built
+   * against ABI 3 (0 = one exchange per sweep) or earlier (no field) gets E = 1, so a loop of one
+   * sweep_local / exchange / sweep_finish round per sweep stays a whole sweep; brr_session_sweep and
+   * distributed.HostExchange query brr_session_exchanges_per_sweep() and run E rounds. */
   int32_t exchanges_per_sweep;
 } brr_options;
 
 void brr_options_default(brr_options *opt);
+/* the options the library uses for a caller's struct (defaults for a NULL pointer, the ABI-version
+ * upgrade of an older struct applied) */
+void brr_options_effective(const brr_options *in, brr_options *out);
 const char *brr_last_error(void);
 int brr_device_count(void);
+/* free and total device memory of a HIP device in bytes (a caller sizing its shards; a session whose
+ * buffers do not fit fails at brr_session_create with the sizes in brr_last_error()) */
+int brr_device_memory(int32_t device, int64_t *free_bytes, int64_t *total_bytes);
 
 /* ---------------- one-shot drop-in entry points (reference signatures) ---------------- */
 int brr_BayesRSamplerV2(const char *outputFile, int seed, int max_iterations, int burn_in,

@@ -10,7 +10,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -q --maxfail 8 --timeout 150 
   > gpurun_out/${TAG}_gpu_tests.log 2>&1
 rc=$?
 tail -3 gpurun_out/${TAG}_gpu_tests.log
-[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+[ $rc -eq 0 ] || { echo "GPU TESTS FAILED rc=$rc"; exit 1; }
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 \
   || { echo "smoke failed"; tail -20 gpurun_out/${TAG}_smoke.log; exit 1; }
 tail -2 gpurun_out/${TAG}_smoke.log

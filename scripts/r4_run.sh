@@ -11,7 +11,7 @@ if [ "${TESTS:-1}" = 1 ]; then
     ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/${TAG}_gpu_tests.log 2>&1
   rc=$?
   tail -15 gpurun_out/${TAG}_gpu_tests.log
-  [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+  [ $rc -eq 0 ] || { echo "GPU TESTS FAILED rc=$rc"; exit 1; }
 fi
 for cfg in $RUNS; do
   name=${cfg%%:*}; args=$(echo ${cfg#*:} | tr ',' ' ')

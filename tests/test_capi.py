@@ -86,12 +86,12 @@ def test_header_compiles_as_c(tmp_path):
 
 def test_options_struct_layout(brr, tmp_path):
     # the ctypes mirror has the C compiler's layout of brr_options (ABI 2: row-shard fields, ABI 3:
-    # exchanges_per_sweep)
+    # exchanges_per_sweep; ABI 4: 0 there means automatic)
     from bayesrrcpp_amd import _lib
     o = _lib.options()
-    assert o.abi_version == _lib.ABI_VERSION == 3
+    assert o.abi_version == _lib.ABI_VERSION == 4
     assert o.row_shard_count == 1 and o.row_shard_rank == 0 and o.N_total == 0
-    assert o.exchanges_per_sweep == 0  # automatic (column shards: E = shard count)
+    assert o.exchanges_per_sweep == 0  # automatic (column shards: E = 8, capped at the blocks per shard)
     src = tmp_path / "lay.c"
     fields = [f[0] for f in _lib.Options._fields_]
     src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "brr.h"\nint main(void){'
@@ -105,3 +105,23 @@ def test_options_struct_layout(brr, tmp_path):
     got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     assert got[0] == C.sizeof(_lib.Options)
     assert got[1:] == [getattr(_lib.Options, f).offset for f in fields]
+
+
+@pytest.mark.parametrize("abi,given,want", [(4, 0, 0), (4, 3, 3), (3, 0, 1), (3, 5, 5), (2, 7, 1), (1, 7, 1)])
+def test_older_abi_keeps_one_exchange_per_sweep(brr, abi, given, want):
+    # ABI 4 made exchanges_per_sweep = 0 automatic (E = 8); a caller built against ABI 3 (0 = one
+    # exchange per sweep) or earlier (no such field: whatever follows its struct is not read) keeps
+    # E = 1, so its one sweep_local / exchange / sweep_finish round per sweep stays a whole sweep
+    from bayesrrcpp_amd import _lib
+    L = brr.lib()
+    o = _lib.options(block_size=256, shard_count=2)
+    o.abi_version, o.exchanges_per_sweep = abi, given
+    out = _lib.Options()
+    L.brr_options_effective(C.byref(o), C.byref(out))
+    assert out.abi_version == _lib.ABI_VERSION
+    assert out.exchanges_per_sweep == want
+    assert out.shard_count == 2
+    assert out.block_size == 256
+    assert out.row_shard_count == 1
+    L.brr_options_effective(None, C.byref(out))  # NULL: the defaults
+    assert out.exchanges_per_sweep == 0 and out.shard_count == 1

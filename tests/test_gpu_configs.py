@@ -46,37 +46,38 @@ def test_c1_oneshot_at_stated_shape(brr, oracle_mod, require_gpu, tmp_path):
 def test_c5_rank_workload(brr, require_gpu):
     from bayesrrcpp_amd import _lib as L
     N, P_loc, M_tot, R = 500_000, 125_000, 1_000_000, 8
-    s = brr.Session(L.MODEL_V2, N, P_loc, K=4, M_total=M_tot, col_offset=0, shard_rank=0, shard_count=R)
-    assert s.block_size == 512
-    s.synthesize(20261015, 0.5, -1)
-    # Y from this shard's genetic values (the other shards' parts zero), standardised
-    s.synth_y(s.synth_partial_y(), 20261015, 0.5)
-    s.set_bayesr(**HYP, cva=CVA)
-    s.init(1)
-    Y = s.vector(L.EPS).copy()  # eps after init = Y - 0 - X 0
-    s.exchange_buffers()
-    E = s.exchanges_per_sweep
-    assert E == 8  # automatic
-    for it in range(10):
-        for e in range(E):
-            eps0, mu0 = s.vector(L.EPS), s.scalar(L.MU)
-            s.sweep_local()
-            mu1 = s.scalar(L.MU)
-            # the sweep start's shift (src/BayesRv2.cpp:177-179); later segments start from eps as is
-            eps_start = (eps0 + mu0) - mu1 if e == 0 else eps0
-            dE, stats = s.exchange_get()
-            eps_loc = s.vector(L.EPS)
-            assert np.array_equal(dE, eps_loc - eps_start), f"exchange buffer != eps_local - eps_start at {it}.{e}"
-            if e < E - 1:
-                assert not np.any(stats), "statistics follow the last segment only"
-            # the seven other ranks contribute zero deltas and zero statistics: the sum is this rank's
-            s.exchange_set(dE, stats)
-            s.sweep_finish()
-        assert s.iteration == it + 1
-    beta, eps, mu = s.vector(L.BETA), s.vector(L.EPS), s.scalar(L.MU)
-    xb = s.linear_predictor()
-    sigmaE = s.scalar(L.SIGMAE)
-    s.close()  # frees the 250 GB of X
+    # the 250 GB of X go at the with-block's end, also when an assertion inside fails (a retained
+    # session made the next 200 GB create fail, gpurun_out/r04rn_tests.log)
+    with brr.Session(L.MODEL_V2, N, P_loc, K=4, M_total=M_tot, col_offset=0, shard_rank=0, shard_count=R) as s:
+        assert s.block_size == 512
+        s.synthesize(20261015, 0.5, -1)
+        # Y from this shard's genetic values (the other shards' parts zero), standardised
+        s.synth_y(s.synth_partial_y(), 20261015, 0.5)
+        s.set_bayesr(**HYP, cva=CVA)
+        s.init(1)
+        Y = s.vector(L.EPS).copy()  # eps after init = Y - 0 - X 0
+        s.exchange_buffers()
+        E = s.exchanges_per_sweep
+        assert E == 8  # automatic
+        for it in range(10):
+            for e in range(E):
+                eps0, mu0 = s.vector(L.EPS), s.scalar(L.MU)
+                s.sweep_local()
+                mu1 = s.scalar(L.MU)
+                # the sweep start's shift (src/BayesRv2.cpp:177-179); later segments start from eps as is
+                eps_start = (eps0 + mu0) - mu1 if e == 0 else eps0
+                dE, stats = s.exchange_get()
+                eps_loc = s.vector(L.EPS)
+                assert np.array_equal(dE, eps_loc - eps_start), f"exchange buffer != eps_local - eps_start at {it}.{e}"
+                if e < E - 1:
+                    assert not np.any(stats), "statistics follow the last segment only"
+                # the seven other ranks contribute zero deltas and zero statistics: the sum is this rank's
+                s.exchange_set(dE, stats)
+                s.sweep_finish()
+            assert s.iteration == it + 1
+        beta, eps, mu = s.vector(L.BETA), s.vector(L.EPS), s.scalar(L.MU)
+        xb = s.linear_predictor()
+        sigmaE = s.scalar(L.SIGMAE)
     nz = int(np.count_nonzero(beta))
     assert 0 < nz < P_loc
     ref = Y - mu - xb

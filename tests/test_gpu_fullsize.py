@@ -27,11 +27,10 @@ def _c2_session(brr, L, x_storage):
 def test_c2_residual_invariant(brr, oracle_mod, require_gpu):
     from bayesrrcpp_amd import _lib as L
     O = oracle_mod
-    s = _c2_session(brr, L, L.X_F32)
-    Y = s.vector(L.EPS).copy()  # eps after init = Y - 0 - X 0
-    s.sweep(10)
-    beta, eps, mu = s.vector(L.BETA), s.vector(L.EPS), s.scalar(L.MU)
-    s.close()  # frees the 200 GB of X before the next session
+    with _c2_session(brr, L, L.X_F32) as s:  # the 200 GB of X go at the block's end, also on a failure
+        Y = s.vector(L.EPS).copy()  # eps after init = Y - 0 - X 0
+        s.sweep(10)
+        beta, eps, mu = s.vector(L.BETA), s.vector(L.EPS), s.scalar(L.MU)
     nz = np.nonzero(beta)[0]
     assert 0 < nz.size < 20_000, nz.size
     xb = np.zeros(N)
@@ -46,18 +45,17 @@ def test_c2_2bit_chain_identical(brr, require_gpu, monkeypatch):
     from bayesrrcpp_amd import _lib as L
     monkeypatch.setenv("BRR_LAG", "2")  # both storages on the f32 default pipeline (lag 2)
     traj = []
-    s = _c2_session(brr, L, L.X_F32)
-    for _ in range(4):
-        s.sweep(1)
-        traj.append((s.vector(L.BETA), s.vector(L.COMP), s.vector(L.EPS), s.scalar(L.SIGMAE), s.scalar(L.MU)))
-    s.close()  # frees the 200 GB of X before the next session
-    s = _c2_session(brr, L, L.X_2BIT)
-    for it, (b, c, e, se, mu) in enumerate(traj):
-        s.sweep(1)
-        assert np.array_equal(s.vector(L.BETA), b), f"beta differs at sweep {it}"
-        assert np.array_equal(s.vector(L.COMP), c), f"comp differs at sweep {it}"
-        assert np.array_equal(s.vector(L.EPS), e), f"eps differs at sweep {it}"
-        assert s.scalar(L.SIGMAE) == se and s.scalar(L.MU) == mu, f"scalars differ at sweep {it}"
+    with _c2_session(brr, L, L.X_F32) as s:  # frees the 200 GB of X before the next session
+        for _ in range(4):
+            s.sweep(1)
+            traj.append((s.vector(L.BETA), s.vector(L.COMP), s.vector(L.EPS), s.scalar(L.SIGMAE), s.scalar(L.MU)))
+    with _c2_session(brr, L, L.X_2BIT) as s:
+        for it, (b, c, e, se, mu) in enumerate(traj):
+            s.sweep(1)
+            assert np.array_equal(s.vector(L.BETA), b), f"beta differs at sweep {it}"
+            assert np.array_equal(s.vector(L.COMP), c), f"comp differs at sweep {it}"
+            assert np.array_equal(s.vector(L.EPS), e), f"eps differs at sweep {it}"
+            assert s.scalar(L.SIGMAE) == se and s.scalar(L.MU) == mu, f"scalars differ at sweep {it}"
 
 
 def test_linear_predictor_small(brr, oracle_mod, require_gpu):
@@ -96,17 +94,16 @@ def test_c3_residual_invariant(brr, require_gpu):
     group's pi a probability vector, v counts add up to P."""
     from bayesrrcpp_amd import _lib as L
     G = 22
-    s = brr.Session(L.MODEL_GROUPS, N, P, K=4, groups=G, F=1)
-    s.synthesize(DS, 0.5, -1)
-    s.set_bayesr(**HYP, cva=np.tile(CVA, (G, 1)), gAssign=(np.arange(P) * G // P).astype(np.int32))
-    s.set_fixed(np.zeros((N, 1)))
-    s.init(1)
-    Y = s.vector(L.EPS).copy()  # eps after init = Y - mu with mu = 0 (BayesRv2Groups.cpp:203)
-    s.sweep(10)
-    err = _invariant(s, L, Y)
-    sgg, pi, vc = s.vector(L.SIGMAGG), s.vector(L.PI).reshape(G, 4), s.vector(L.VCOUNT)
-    nz = int(np.count_nonzero(s.vector(L.BETA)))
-    s.close()
+    with brr.Session(L.MODEL_GROUPS, N, P, K=4, groups=G, F=1) as s:
+        s.synthesize(DS, 0.5, -1)
+        s.set_bayesr(**HYP, cva=np.tile(CVA, (G, 1)), gAssign=(np.arange(P) * G // P).astype(np.int32))
+        s.set_fixed(np.zeros((N, 1)))
+        s.init(1)
+        Y = s.vector(L.EPS).copy()  # eps after init = Y - mu with mu = 0 (BayesRv2Groups.cpp:203)
+        s.sweep(10)
+        err = _invariant(s, L, Y)
+        sgg, pi, vc = s.vector(L.SIGMAGG), s.vector(L.PI).reshape(G, 4), s.vector(L.VCOUNT)
+        nz = int(np.count_nonzero(s.vector(L.BETA)))
     assert err < 1e-9, err
     assert np.all(np.isfinite(sgg)) and np.all(sgg > 0)
     assert np.all(pi >= 0) and np.allclose(pi.sum(1), 1.0, rtol=1e-12)
@@ -118,17 +115,16 @@ def test_c4_residual_invariant(brr, require_gpu):
     10 sweeps eps = Y - mu - X beta (HorseshoeR.cpp:186,210-212,224,238) within 1e-9; every marker moved
     (Horseshoe resamples all); lambda, tau, c2, eta finite and positive (HorseshoeR.cpp:242-253)."""
     from bayesrrcpp_amd import _lib as L
-    s = brr.Session(L.MODEL_HORSESHOE, N, P, K=1)
-    s.synthesize(DS, 0.5, -1)
-    s.set_horseshoe(A=(1 / N ** 0.5) * 1500 / (P - 1500), v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0, c2=1.0,
-                    vC=10.0, sC=10.0)
-    s.init(1)
-    Y = s.vector(L.EPS).copy()  # eps after init = Y - mu - X 0 (HorseshoeR.cpp:186)
-    s.sweep(10)
-    err = _invariant(s, L, Y)
-    lam, beta = s.vector(L.LAMBDA), s.vector(L.BETA)
-    sc = [s.scalar(w) for w in (L.TAU, L.C2, L.ETA, L.SIGMAE)]
-    s.close()
+    with brr.Session(L.MODEL_HORSESHOE, N, P, K=1) as s:
+        s.synthesize(DS, 0.5, -1)
+        s.set_horseshoe(A=(1 / N ** 0.5) * 1500 / (P - 1500), v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0, c2=1.0,
+                        vC=10.0, sC=10.0)
+        s.init(1)
+        Y = s.vector(L.EPS).copy()  # eps after init = Y - mu - X 0 (HorseshoeR.cpp:186)
+        s.sweep(10)
+        err = _invariant(s, L, Y)
+        lam, beta = s.vector(L.LAMBDA), s.vector(L.BETA)
+        sc = [s.scalar(w) for w in (L.TAU, L.C2, L.ETA, L.SIGMAE)]
     assert err < 1e-9, err
     assert np.count_nonzero(beta) == P
     assert np.all(np.isfinite(lam)) and np.all(lam > 0)

@@ -1,0 +1,80 @@
+"""A session create that cannot fit in HBM while another session is alive fails cleanly: NULL from
+brr_session_create with the sizes in brr_last_error(), and the library keeps working afterwards.
+
+Round 4's GPU log (gpurun_out/r04rn_tests.log) ended in a host SIGSEGV inside brr_session_create:
+the C5-rank test (250 GB of X) had failed an assertion and its session stayed alive in the
+traceback, so the next test's 200 GB create could not fit.  Both paths are run in a child process
+(a crash there fails this test instead of ending the GPU suite):
+* the preflight (default): free HBM checked against the big buffers before anything is allocated;
+* BRR_NO_MEM_PREFLIGHT=1: the allocations themselves fail, and every failure return of create
+  destroys the partly built session (brr_session.cpp: brr_session_create, ~brr_session).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import json, sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from bayesrrcpp_amd import _lib as L
+from bayesrrcpp_amd.session import Session
+out = {}
+free0, total = L.device_memory(0)
+out["free0"], out["total"] = free0, total
+# the session kept alive: ~40 % of the device (N = 100,000 rows of f32 X)
+N = 100_000
+M_alive = int(0.4 * total / (4 * 100_096)) // 512 * 512
+a = Session(L.MODEL_V2, N, M_alive, K=4)
+free1, _ = L.device_memory(0)
+out["free_with_alive"] = free1
+# a second session whose X alone is 10 GB more than what is free
+M_big = int((free1 + 10e9) / (4 * 100_096)) // 512 * 512 + 512
+try:
+    Session(L.MODEL_V2, N, M_big, K=4)
+    out["big"] = "created"
+except L.BrrError as e:
+    out["big"] = "failed"
+    out["msg"] = str(e)
+free2, _ = L.device_memory(0)
+out["free_after"] = free2
+a.close()
+# the library still runs a chain afterwards
+rng = np.random.default_rng(3)
+X = rng.normal(size=(500, 300)).astype(np.float32)
+Y = X[:, :5].sum(1) + rng.normal(size=500)
+Y = (Y - Y.mean()) / Y.std()
+with Session(L.MODEL_V2, 500, 300, K=4, block_size=128) as s:
+    s.upload_x(X).set_y(Y)
+    s.set_bayesr(0.0001, 0.0001, 0.0001, 0.0001, 0.0001, np.array([0.0001, 0.001, 0.01]))
+    s.init(1)
+    s.sweep(3)
+    out["sigmaE"] = s.scalar(L.SIGMAE)
+print("RESULT " + json.dumps(out))
+"""
+
+
+@pytest.mark.parametrize("preflight", [True, False])
+def test_create_beyond_free_hbm_fails_cleanly(brr, require_gpu, preflight):
+    env = dict(os.environ)
+    if not preflight:
+        env["BRR_NO_MEM_PREFLIGHT"] = "1"
+    r = subprocess.run([sys.executable, "-c", CHILD, REPO], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, f"child exited {r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}"
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
+    out = json.loads(line[len("RESULT "):])
+    assert out["big"] == "failed", out
+    if preflight:
+        assert "GB free" in out["msg"] and "needs" in out["msg"], out["msg"]
+    else:
+        assert "hipMalloc" in out["msg"], out["msg"]
+    # nothing of the failed session stays allocated
+    assert abs(out["free_after"] - out["free_with_alive"]) < 1e9, out
+    assert out["sigmaE"] > 0
