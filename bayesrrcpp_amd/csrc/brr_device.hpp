@@ -59,10 +59,8 @@ struct Scal {
   unsigned long long nch_mark;   // n_changed at the end of the previous sweep
   int prof_on;                   // diagnostics: k_solve phase timers on
   int pad2;
-  unsigned long long prof[24];   // k_solve phase totals (wall_clock64 ticks, 100 MHz), counters;
-                                 // [16]: streamer boundaries served by the list prefetch;
-                                 // [20..22] (always counted) prefetch helpers: blocks prefetched, blocks
-                                 // found too late, helper launches off the solver's XCD
+  unsigned long long prof[20];   // k_solve phase totals (wall_clock64 ticks, 100 MHz), counters;
+                                 // [16]: streamer boundaries served by the list prefetch
 };
 
 struct Hyper {
@@ -80,8 +78,7 @@ enum SyncWord : int {
   SY_ERR = 160,    // a bounded wait expired; SY_ERR + 1..4: site, target, value seen, workgroup
   SY_ARRIVE = 192, // persistent streamer workgroups that started (session total)
   SY_TS = 224,     // diagnostics: 64-bit wall-clock stamps (see brr_session.cpp)
-  SY_XCC = 256,    // the fused solver workgroup's XCD (HW_REG_XCC_ID + 1), for its prefetch helpers
-  SY_WORDS = 288
+  SY_WORDS = 256
 };
 
 // Pipeline rings: partial-dot slabs, their arrival counters and reduction counts cycle over
@@ -110,7 +107,6 @@ struct Dev {
                     // write (reduce_role); the solver's phase A then forms none
   int slab_storage; // the partial dots are indexed by in-block storage index, not visit position
                     // (fused sweep on 2-bit code tiles)
-  int nhelp;        // (fused sweep) prefetch helper workgroups beside the solver (k_sweep_solve, helper_role)
   uint64_t seed;
   Hyper hyp;
   const float *X;      // f32 storage (x_storage BRR_X_F32), else nullptr

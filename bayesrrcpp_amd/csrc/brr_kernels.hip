@@ -163,9 +163,8 @@ __device__ __forceinline__ int ld_sc1_int(const int *p) {
 // that will use it next until its reducer overwrites it with the dot -- a signalling-NaN bit pattern
 // that arithmetic never produces (it yields quiet NaNs), carrying the block's session-wide epoch
 // (Dev::sbase + s) so that a stale value of an earlier block is never mistaken for ready data.
-constexpr unsigned long long SENTINEL_HI = 0x7FF40000ull;  // the high word of every sentinel
 __host__ __device__ inline unsigned long long slab_sentinel(int epoch) {
-  return (SENTINEL_HI << 32) | (unsigned long long)(unsigned)epoch;
+  return 0x7FF4000000000000ull | (unsigned long long)(unsigned)epoch;
 }
 
 // Bounded wait (one lane) for a device counter published by a kernel running concurrently on
@@ -2502,6 +2501,11 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
       // the dots are by visit position, or by in-block (storage) index when the 2-bit streamers
       // read the block in storage order (a permutation of 0 .. bs-1; columns bs .. B-1 are unread)
       const int sidx = pos < bs && d.slab_storage ? Lgi[pos] : pos;
+      // (this block's sentinel only: a stale one of another epoch cannot be here -- after a failed census
+      // the error flag makes every later fused launch leave at its census until the host has switched
+      // the session to the per-block kernels, which use no sentinels.  Testing for any sentinel instead
+      // cost the B = 512 solver 16 more spilled VGPRs.)
+      const unsigned long long sent = slab_sentinel(d.sbase + s);
       for (int g0 = 0; g0 < d.NG; g0 += 16) {
         unsigned long long v[16];
         for (uint32_t n = 0;; ++n) {
@@ -2509,9 +2513,7 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
 #pragma unroll
           for (int u = 0; u < 16; ++u) {
             v[u] = g0 + u < d.NG ? ld_sc1_u64(slab2 + (int64_t)(g0 + u) * B + sidx) : 0ull;
-            // any sentinel is "not yet": a stale one of another epoch (a failed launch's slot) waits
-            // into the bounded timeout instead of being summed as data
-            ready = ready && (!persistent || (v[u] >> 32) != (SENTINEL_HI));
+            ready = ready && (!persistent || v[u] != sent);
           }
           if (ready) break;
           if (n > SPIN_MAX) {  // bounded, as wait_geq: the host reports the protocol error
@@ -3782,109 +3784,11 @@ __device__ __forceinline__ bool sweep_census(const Dev &d, int total, int *s_ok)
 }
 
 constexpr int SOLVE_NT = SWEEP_NT;  // the solver workgroup's threads
-
-__device__ __forceinline__ int xcc_id() { return __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 15; }
-
-// Prefetch helper h of nh (Dev::nhelp; workgroup 8 (h + 1) of k_sweep_solve, on the solver's XCD under the
-// observed round-robin placement -- checked against the solver's HW_REG_XCC_ID, speed only).  The solver
-// reads its phase-A sources of block s (per-position constants, Gram and member indices, the resident Gram
-// block, the cross-Gram block of its correction) at one CU's share of a saturated HBM (~25 GB/s: the
-// streamers stream block s+1 right then).  The HBM is quiet between the moment the streamers finish
-// block s (its reducers publish) and the solver's publication of block s-1 (the streamers wait for it):
-// in that window the helper reads the same bytes once, by LDS-DMA into its own LDS, so they sit in the
-// XCD's 4 MB L2 when the solver asks for them (L2 hits: ~3x the per-CU rate).  A helper only reads;
-// nothing waits for it, and a block it reaches too late is skipped.
-template <bool HS, int B>
-__device__ void helper_role(const Dev &d, int h, int nh, char *smem, int *s_go) {
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  constexpr int NW = SOLVE_NT / 64;
-  if (t == 0) {
-    const int same = ld_sc1_int(d.sync + SY_XCC) == xcc_id() + 1;
-    if (!same) atomicAdd(&d.sc->prof[22], 1ull);
-    *s_go = same;
-  }
-  __syncthreads();
-  if (!*s_go) return;
-  const int K = HS ? 1 : d.K, KD = K > 1 ? K - 1 : 0;
-  const int nfield = 4 + K + KD;  // MC_P .. the last den_k (k_prep)
-  const int64_t S = d.nbB;
-  char *dst = smem + wv * 1024;  // (the bytes land in this workgroup's LDS and are never read)
-  for (int s = d.seg0 + 1; s < d.seg1; ++s) {
-    __syncthreads();  // every thread has read *s_go of the previous block
-    if (t == 0) {
-      const int par = s % NPAR;
-      const int tgt = (d.gbase[par] + s / NPAR + 1) * d.gtarget;
-      int go = -1;
-      for (uint32_t n = 0; n < SPIN_MAX; ++n) {
-        if (ld_sc1_int(d.sync + SY_ERR)) break;
-        if ((int)((unsigned)ld_sc1_int(d.sync + SY_PEND) - (unsigned)(d.sbase + s)) >= 0) { go = 0; break; }
-        if ((int)((unsigned)ld_sc1_int(d.sync + SY_GDONE + 32 * par) - (unsigned)tgt) >= 0) { go = 1; break; }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      if (go == 1 && h == 0) atomicAdd(&d.sc->prof[20], 1ull);
-      if (go == 0 && h == 0) atomicAdd(&d.sc->prof[21], 1ull);
-      *s_go = go;
-    }
-    __syncthreads();
-    const int go = *s_go;
-    if (go < 0) return;  // a protocol error, or no progress: nothing more to prefetch
-    if (go == 0) continue;
-    const int gb = d.gblk[s];
-    const int64_t q0 = (int64_t)s * B;
-    // 1 KiB pieces: the constants (B doubles per field), the Gram indices and members (B ints each),
-    // then (resident solver) the Gram block and the cross-Gram block of the correction
-    const int pc_f = B * 8 / 1024, n_f = nfield * pc_f;
-    const int pc_i = B * 4 / 1024 > 0 ? B * 4 / 1024 : 1, n_i = 2 * pc_i;
-    const bool res = B <= RESIDENT_BMAX;
-    const int pc_g = res ? B * B * 8 / 1024 : 0;
-    const char *xg = nullptr;
-    if (res && !d.rcorr && s - 1 >= d.seg0) {
-      const int gp = d.gblk[s - 1];
-      xg = reinterpret_cast<const char *>((gb == (gp + 1) % d.nb) ? d.xgram + (int64_t)gp * B * B
-                                                                   : d.xgramT + (int64_t)gb * B * B);
-    }
-    const int n_x = xg ? pc_g : 0;
-    const int ntot = n_f + n_i + pc_g + n_x;
-    for (int c = h + nh * wv; c < ntot; c += nh * NW) {
-      const char *src;
-      int lim = 1024;  // bytes of this piece
-      if (c < n_f) {
-        const int f = c / pc_f, o = c % pc_f;
-        src = reinterpret_cast<const char *>(d.mc + (int64_t)f * S + q0) + o * 1024;
-      } else if (c < n_f + n_i) {
-        const int f = (c - n_f) / pc_i, o = (c - n_f) % pc_i;
-        src = reinterpret_cast<const char *>((f == 0 ? d.gidx : d.member) + q0) + o * 1024;
-        lim = min(1024, B * 4);
-      } else if (c < n_f + n_i + pc_g) {
-        src = reinterpret_cast<const char *>(d.gram + (int64_t)gb * B * B) + (int64_t)(c - n_f - n_i) * 1024;
-      } else {
-        src = xg + (int64_t)(c - n_f - n_i - pc_g) * 1024;
-      }
-      if (lane * 16 < lim)
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + lane * 16),
-                                         (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // landed: the lines are in the L2
-  }
-}
-
-// grid: workgroup 0 = the solver; workgroups 8, 16, .., 8 nhelp = prefetch helpers (Dev::nhelp); the
-// others leave at once, before the census (which counts 1 + nhelp of this kernel)
 template <bool HS, int B>
 __global__ __launch_bounds__(SOLVE_NT, 1) void k_sweep_solve(Dev d, uint32_t it, int nslot, int total) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_ok;
-  const int b = blockIdx.x;
-  if (b > 0 && ((b & 7) != 0 || (b >> 3) > d.nhelp)) return;
-  if (b == 0 && d.nhelp > 0 && threadIdx.x == 0) {
-    st_sc1_int(d.sync + SY_XCC, xcc_id() + 1);  // before this workgroup's census arrival
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
   if (!sweep_census(d, total, &s_ok)) return;
-  if (b > 0) {
-    helper_role<HS, B>(d, (b >> 3) - 1, d.nhelp, smem, &s_ok);
-    return;
-  }
   solver_role<HS, B, SOLVE_NT>(d, it, nslot, smem);
 }
 
@@ -3898,7 +3802,7 @@ __global__ __launch_bounds__(NT, 1) void k_sweep_stream(Dev d, int nsg, int rpw,
   __shared__ int s_np[2];
   __shared__ int s_ok;
   __shared__ int s_pf[NT / 64];
-  if (!sweep_census(d, nsg + 1 + nred + d.nhelp, &s_ok)) return;
+  if (!sweep_census(d, nsg + 1 + nred, &s_ok)) return;
   if ((int)blockIdx.x >= nsg) {
     reduce_role<NT>(d, (int)blockIdx.x - nsg, nsg, nred, d.sc->prof_on, reinterpret_cast<double *>(smem));
     return;
@@ -4448,11 +4352,11 @@ hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipS
     const void *fs = solve_kernel(d.model, d.B), *ft = stream_kernel(xv, xv == 1 ? c.stnt : SWEEP_NT);
     if (xv == 2) cc = 1;  // (k_sweep_stream<2> always keeps the cache)
     if (!fs || !ft) return hipErrorInvalidValue;
-    int total = nsg + 1 + nred + d.nhelp;
+    int total = nsg + 1 + nred;
     hipError_t e = hipEventRecord(ev_go, st);
     if (e == hipSuccess) e = hipStreamWaitEvent(st_side, ev_go, 0);
     void *sargs[] = {&dd, &it, &nslot, &total};
-    if (e == hipSuccess) e = hipLaunchKernel(fs, dim3(1 + 8 * d.nhelp), dim3(SOLVE_NT), sargs, (unsigned)c.lds, st);
+    if (e == hipSuccess) e = hipLaunchKernel(fs, dim3(1), dim3(SOLVE_NT), sargs, (unsigned)c.lds, st);
     int pfe = xv == 0 ? c.pfe : 0;
     void *targs[] = {&dd, &nsg, &rpw, &npass, &nred, &cc, &pfe};
     if (e == hipSuccess)

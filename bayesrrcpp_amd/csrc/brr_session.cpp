@@ -386,7 +386,6 @@ int check_device_error(brr_session *s, bool mid_sweep = false) {
     if (sy[SY_ERR + 1] == 5 && s->fused.nsg > 0) {
       s->fused = FusedCfg{};
       s->d.lag = 1;
-      s->d.nhelp = 0;
       // the hand-over counters are cumulative epochs of one pipeline geometry (and the failed
       // sweep advanced none of them): start every epoch again from zero
       const int NC = s->B >= 128 ? s->B / 128 : 1;
@@ -480,7 +479,7 @@ int do_sweep_local(brr_session *s) {
   const bool fused = s->fused.nsg > 0;
   if (s1 > s0 && fused) {
     d.abase = s->abase;  // residency census epoch of this launch
-    s->abase += s->fused.nsg + 1 + s->fused.nred + d.nhelp;
+    s->abase += s->fused.nsg + 1 + s->fused.nred;
     Dev dp = d;
     dp.NG = s->fused.ngroups;  // (1: the reducers write every column's whole sum)
     dp.gtarget = s->fused.nred;
@@ -1248,18 +1247,6 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     if (rows || ref2bit || (pb && pb[0] == '1') || !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused, f32cc))
       s->fused = FusedCfg{};
     if (s->fused.nsg == 0) d.lag = 1;
-    // prefetch helpers beside the persistent solver (k_sweep_solve, helper_role): for the resident-Gram
-    // solver (B <= 128: C3, C4), whose phase-A bytes (Gram + cross-Gram blocks, constants) it otherwise
-    // reads at one CU's share of the saturated HBM; on CUs the geometry leaves idle.  BRR_HELPERS=n
-    // overrides (0: none)
-    {
-      const char *hv = getenv("BRR_HELPERS");
-      int nh = hv ? atoi(hv) : (B <= 128 ? 1 : 0);
-      nh = std::max(0, std::min(nh, 4));
-      if (s->fused.nsg == 0 || !s->fused.split) nh = 0;
-      while (nh > 0 && 1 + nh + s->fused.nsg + s->fused.nred > cus) --nh;
-      d.nhelp = nh;
-    }
     // the persistent solver polls its reduced dots against per-block sentinels (brr_kernels.hip
     // slab_sentinel): slot p starts with block p's
     if (s->fused.nsg > 0 && launch_slab_sentinels(d, (int)(d.slab2_stride / B), s->st) != hipSuccess) {
@@ -1874,9 +1861,6 @@ int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
     case 110: case 111: case 112: case 113: case 114: case 115: case 116: case 117: case 118: case 119:
     case 120: case 121: case 122: case 123: case 124: case 125: case 126: case 127: case 128: case 129:
       *out = (double)sc.prof[which - 110]; return 0;
-    case 132: case 133: case 134:  // prefetch helpers: blocks prefetched, too late, launches off the solver's XCD
-      *out = (double)sc.prof[which - 112]; return 0;
-    case 135: *out = (double)s->d.nhelp; return 0;  // prefetch helper workgroups
     default: set_error("unknown scalar %d", which); return -1;
   }
 }

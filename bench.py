@@ -628,8 +628,6 @@ def main():
             "config": {"workload": cfg["workload"] + (" [2-bit genotype storage, SURVEY 8f3]" if x2 else ""),
                        "x_storage": args.x_storage, "N": N, "P": P, "K": K, "groups": G,
                        "block_size": Bsz, "order": args.order, "fused_stream_wg": int(s.scalar(104)), "code_cache": int(s.scalar(105)), "pipeline_lag": int(s.scalar(106)), "stream_wg_threads": int(diag_scalar(109)), "reducer_wg": int(diag_scalar(131)),
-                       "prefetch_helpers": int(diag_scalar(135)),
-                       "helper_blocks": [int(diag_scalar(132)), int(diag_scalar(133)), int(diag_scalar(134))],
                        "census_failures": int(diag_scalar(130)),
                        "parallelism": (f"row-shard x{world} (exact)" if rows
                                        else f"column-shard rank 0 of {emu} emulated on 1 GPU, {n_ex} exchanges per sweep "
