@@ -520,10 +520,14 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms = dt / args.steps * 1e3
+    # fingerprint of the chain's state after the timed sweeps (A/B runs of library variants that must give
+    # the same chain compare it)
+    import hashlib
+    state_sha = hashlib.sha256(s.vector(L.BETA).tobytes() + s.vector(L.EPS).tobytes()).hexdigest()[:16]
     if diag_scalar(130) > 0:  # the fused sweep fell back to the per-block kernels: say so, loudly
         print(f"bench.py: WARNING: {int(diag_scalar(130))} fused sweep(s) failed the residency census; the "
               "session ran the per-block kernels afterwards (see config.census_failures)", file=sys.stderr)
-    diag = {"slow_steps_per_sweep": s.scalar(100) / (args.warmup + args.steps),
+    diag = {"state_sha16": state_sha, "slow_steps_per_sweep": s.scalar(100) / (args.warmup + args.steps),
             "changed_per_sweep": s.scalar(101) / (args.warmup + args.steps),
             "nonzero_frac": 1.0 - float(s.vector(L.VCOUNT)[0]) / P if model != L.MODEL_HORSESHOE else 1.0}
     value = args.steps / dt  # whole-job sweeps/s (every rank holds a shard of the same sweep)
