@@ -1998,6 +1998,154 @@ __device__ __forceinline__ void chain_bayesr_resident(const Dev &d, int bs, doub
   }
 }
 
+// The same chain in sub-blocks (blocked forward substitution).  Lane l holds positions l + 64 q, so
+// sub-block q (positions 64 q .. 64 q + 63) is one position per lane: a step examines and updates ONE
+// register set per lane (its position in the current sub-block) instead of NS, and the sub-block's
+// changes reach the later sub-blocks' positions in one batch when the sub-block ends (the flush: for
+// each change in chain order, r -= G delta at every later position).  Every position still receives the
+// same subtractions in the same (chain) order as in chain_bayesr_resident, and is decided only after all
+// of them, so the chain is bit-identical to it; the flush's reads are independent of each other (off the
+// step's dependency chain).  scripts/mb_chain_br.hip: 733 against 861 shader cycles per step at B = 128
+// (24 changes per block), bit-identical new betas.
+template <int B>
+__device__ __forceinline__ void chain_bayesr_resident_blk(const Dev &d, int bs, double sigmaE, const double *Lr0,
+                                                          const double *Llo, const double *Lhi, const double *Ldsel,
+                                                          const double *Lsdz, const double *Lbo, double *Lbn,
+                                                          const int *Lfl, int *Lks, const int *Lgi, const double *La,
+                                                          const double *Lden, const double *Lp, const double *Lx2,
+                                                          const double *Lz, const int *Lm, const double *coef,
+                                                          bool prof) {
+#pragma clang fp contract(off)
+  constexpr int NS = B / 64;
+  const int lane = threadIdx.x & 63;
+  double r[NS], lo[NS], hi[NS], dv[NS], iv[NS], sz[NS], bo[NS], bn[NS];
+  int gg[NS], ks[NS];
+  uint32_t act = 0, win = 0, valid = 0, exb = 0;
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    const int pos = lane + 64 * q;
+    const bool in = pos < bs;
+    const int fl = in ? Lfl[pos] : 0;
+    r[q] = in ? Lr0[pos] : 0.0;
+    lo[q] = in ? Llo[pos] : 1.0;
+    hi[q] = in ? Lhi[pos] : -1.0;
+    dv[q] = in ? Ldsel[pos] : 1.0;
+    iv[q] = 1.0 / dv[q];
+    sz[q] = in ? Lsdz[pos] : 0.0;
+    bo[q] = in ? Lbo[pos] : 0.0;
+    bn[q] = bo[q];
+    gg[q] = in ? Lgi[pos] : B - 1;  // past the end: an unused Gram index (zero row and column)
+    ks[q] = fl & 0xFF;
+    const double tt = r[q] * r[q];
+    valid |= (uint32_t)in << q;
+    act |= (uint32_t)(in && (fl & PF_LIKELY)) << q;
+    exb |= (uint32_t)(in && (fl & PF_EX)) << q;
+    win |= (uint32_t)(in && tt >= lo[q] && tt <= hi[q]) << q;
+  }
+  int nslow = 0, nsteps = 0, nref = 0;
+  uint64_t tslow = 0;
+  const uint64_t tl0 = prof ? wall_clock64() : 0;
+  static_for<NS>([&](auto kc) __attribute__((always_inline)) {
+    constexpr int k = decltype(kc)::value;
+    constexpr uint32_t bk = 1u << k;
+    if (64 * k >= bs) return;
+    int i = 64 * k;                   // the next position to examine
+    int np = 0, pgi = 0;              // this sub-block's changes: lane c holds change c's Gram index
+    double pdl = 0.0;                 // and its delta
+    while (true) {
+      const bool mine = (lane + 64 * k >= i) && ((valid & (act | ~win | exb) & bk) != 0);
+      // speculative new beta of this lane's position (BayesRv2.cpp:226-230), every arm evaluated and selected
+      const double qv = quot_rn(r[k], dv[k], iv[k]) + sz[k];
+      const double bnl = ks[k] == 0 ? 0.0 : (ks[k] == FALLTHROUGH ? bo[k] : qv);
+      const int fastl = (int)(((win & ~exb) >> k) & 1u);
+      const uint64_t bal = __ballot(mine);
+      if (!bal) break;  // the rest of the sub-block keeps its decisions
+      const int L = __builtin_ctzll(bal);
+      const int first = 64 * k + L;  // wave-uniform
+      const int gif = __builtin_amdgcn_readlane(gg[k], L);
+      double delta;
+      if (__builtin_expect(__builtin_amdgcn_readlane(fastl, L) != 0, 1)) {
+        delta = readlane_f64(bnl - bo[k], L);
+        bn[k] = lane == L ? bnl : bn[k];
+      } else {
+        const uint64_t ts0 = prof ? wall_clock64() : 0;
+        const double rf = readlane_f64(r[k], L);
+        const bool exf = (__builtin_amdgcn_readlane((int)exb, L) >> k) & 1;
+        if (!exf) {
+          // outside its window: re-decide at the current num, then re-examine
+          FastDec o = decide_pos_ool(d.gAssign, d.sigmaGG, d.pi, d.cva, d.G, d.K, rf, La + first, Lden + first, B, sigmaE,
+                                     Lp[first], Lx2[first], Lm[first]);
+          const bool lk = o.ex || !(o.k == FALLTHROUGH || (o.k == 0 && readlane_f64(bo[k], L) == 0.0));
+          const double dsel = (!o.ex && o.k >= 1 && o.k != FALLTHROUGH) ? Lden[(o.k - 1) * B + first] : 1.0;
+          const double sdz = sqrt(sigmaE / dsel) * Lz[first];
+          if (lane == L) {
+            lo[k] = o.lo; hi[k] = o.hi; ks[k] = o.k; dv[k] = dsel; iv[k] = 1.0 / dsel; sz[k] = sdz;
+            act = (act & ~bk) | ((uint32_t)lk << k);
+            win = (win & ~bk) | ((uint32_t)(!o.ex) << k);
+            exb = (exb & ~bk) | ((uint32_t)o.ex << k);
+          }
+          ++nref;
+          if (prof) tslow += wall_clock64() - ts0;
+          continue;
+        }
+        const double bof = readlane_f64(bo[k], L);
+        const int m = Lm[first];
+        const int g = d.gAssign ? d.gAssign[m] : 0;
+        Decision dc = decide_bayesr_ool(rf, Lx2[first], sigmaE, d.sigmaGG[g], d.pi + (int64_t)g * d.K, d.cva + g, d.G,
+                                        d.K, Lp[first], false);
+        const double bnf = dc.k == 0 ? 0.0 : (dc.k == FALLTHROUGH ? bof : rf / dc.denom + sqrt(sigmaE / dc.denom) * Lz[first]);
+        if (lane == L) { bn[k] = bnf; ks[k] = dc.k; }
+        delta = bnf - bof;
+        ++nslow;
+        if (prof) tslow += wall_clock64() - ts0;
+      }
+      // the sub-block's later positions subtract G delta now (the raw Gram block is in LDS); the later
+      // sub-blocks' positions at the flush
+      {
+        const double g = coef[(int64_t)gif * B + gg[k]];
+        const bool later = lane > L && (valid & bk);
+        r[k] = later ? r[k] - g * delta : r[k];
+        const double tt = r[k] * r[k];
+        win = (win & ~bk) | ((uint32_t)(tt >= lo[k] && tt <= hi[k]) << k);
+      }
+      if (k + 1 < NS && delta != 0.0) {  // (a zero delta subtracts exactly nothing)
+        pgi = lane == np ? gif : pgi;
+        pdl = lane == np ? delta : pdl;
+        ++np;
+      }
+      i = first + 1;
+      ++nsteps;
+    }
+    if constexpr (k + 1 < NS) {
+      // flush: this sub-block's changes, in chain order, into every later position
+      for (int c = 0; c < np; ++c) {
+        const int gic = __builtin_amdgcn_readlane(pgi, c);
+        const double dc = readlane_f64(pdl, c);
+        const double *row = coef + (int64_t)gic * B;
+#pragma unroll
+        for (int q = k + 1; q < NS; ++q) r[q] = r[q] - row[gg[q]] * dc;
+      }
+#pragma unroll
+      for (int q = k + 1; q < NS; ++q) {
+        const double tt = r[q] * r[q];
+        win = (win & ~(1u << q)) | ((uint32_t)(((valid >> q) & 1u) && tt >= lo[q] && tt <= hi[q]) << q);
+      }
+    }
+  });
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    const int pos = lane + 64 * q;
+    if (pos < bs) { Lbn[pos] = bn[q]; Lks[pos] = ks[q]; }
+  }
+  if (lane == 0 && nslow) atomicAdd(&d.sc->n_slow, (unsigned long long)nslow);
+  if (prof && lane == 0) {
+    atomicAdd(&d.sc->prof[6], (unsigned long long)nsteps);
+    atomicAdd(&d.sc->prof[7], (unsigned long long)nref);
+    atomicAdd(&d.sc->prof[8], (unsigned long long)tslow);                  // solve_refresh_us: slow paths
+    atomicAdd(&d.sc->prof[9], (unsigned long long)(wall_clock64() - tl0));  // solve_correct_us: whole loop
+  }
+}
+
 // Serial chain, BayesR family, for blocks whose Gram block does not fit in LDS (B = 256, 512): lane
 // l holds positions l NS .. l NS + NS-1 with num and its decision window in registers; the Gram rows
 // are the raw rows of the positions predicted to change (static LDS slots, then the ring the idle
@@ -2230,6 +2378,10 @@ __device__ __attribute__((noinline)) void chain_bayesr_call(
                            from_lds(Lbo), from_lds(Lbn), from_lds(Lfl), from_lds(Lks), from_lds(Lgi), from_lds(La),
                            from_lds(Lden), from_lds(Lp), from_lds(Lx2), from_lds(Lz), from_lds(Lm), from_lds(coef), prof);
 }
+
+#ifndef BRR_CHAIN_BLK
+#define BRR_CHAIN_BLK 1  // the resident BayesR chain in sub-blocks of 64 positions (chain_bayesr_resident_blk); 0: per step
+#endif
 
 #ifndef BRR_EARLY_GRAM
 #define BRR_EARLY_GRAM 0
@@ -2631,7 +2783,10 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
           atomicAdd(&d.sc->prof[12], (unsigned long long)(__builtin_amdgcn_s_memtime() - tq0));  // chain loop, shader clocks
         }
       } else {
-#if BRR_CHAIN_INLINE || !BRR_BAYESR_CHAIN_CALL
+#if BRR_CHAIN_BLK
+        chain_bayesr_resident_blk<B>(d, bs, sigmaE, Lr0, Llo, Lhi, Ldsel, Lsdz, Lbo, Lbn, Lfl, Lks, Lgi, La, Lden, Lp,
+                                     Lx2, Lz, Lm, slots, prof);
+#elif BRR_CHAIN_INLINE || !BRR_BAYESR_CHAIN_CALL
         chain_bayesr_resident<B>(d, bs, sigmaE, Lr0, Llo, Lhi, Ldsel, Lsdz, Lbo, Lbn, Lfl, Lks, Lgi, La, Lden, Lp,
                                  Lx2, Lz, Lm, slots, prof);
 #else

@@ -1,17 +1,20 @@
-// Microbenchmark of the BayesR resident serial chain (chain_bayesr_resident in
+// Microbenchmark of the BayesR resident serial chain, per-step form (chain_bayesr_resident) against the
+// sub-block form (chain_bayesr_resident_blk; both in
 // bayesrrcpp_amd/csrc/brr_kernels.hip) on an idle GPU: shader cycles per chain step for B = 128
 // with `nact` positions predicted to change (C3-like: ~24 per block) and every position inside its
 // decision window (the fast path), one wave, Gram block in LDS -- to separate the chain's own cost
 // from the fused kernel's context.  Values are checked against a host forward substitution.
+// The two forms must give bit-identical new betas (checked).
 // hipcc --offload-arch=gfx950 -O3 -std=c++17 -I bayesrrcpp_amd/csrc scripts/mb_chain_br.hip -o scripts/mb_chain_br.bin
 #include "../bayesrrcpp_amd/csrc/brr_kernels.hip"
 
 #include <cstdio>
+#include <cstring>
 #include <vector>
 
 using namespace brr;
 
-template <int B>
+template <int B, int BLK>
 __global__ __launch_bounds__(512, 1) void k_mb_br(Dev d, const double *G, const int *gi, const double *r0, const double *D, const double *sdz,
                         const double *bo, const int *fl, double *bn, unsigned long long *cyc, int reps, int bs) {
   extern __shared__ double sm[];
@@ -55,8 +58,12 @@ __global__ __launch_bounds__(512, 1) void k_mb_br(Dev d, const double *G, const 
     for (int r = 0; r < reps; ++r) {
       Lr0[l] = ra; Lr0[l + 64] = rb; Lbn[l] = ba; Lbn[l + 64] = bb; Lfl[l] = fa; Lfl[l + 64] = fb;
       __builtin_amdgcn_wave_barrier();
-      chain_bayesr_resident<B>(d, bs, 1.0, Lr0, Llo, Lhi, Ld, Lz, Lbo, Lbn, Lfl, Lks, Lgi, La, Lden, Lp, Lx2, Lzz, Lm,
-                               coef, false);
+      if constexpr (BLK)
+        chain_bayesr_resident_blk<B>(d, bs, 1.0, Lr0, Llo, Lhi, Ld, Lz, Lbo, Lbn, Lfl, Lks, Lgi, La, Lden, Lp, Lx2, Lzz,
+                                     Lm, coef, false);
+      else
+        chain_bayesr_resident<B>(d, bs, 1.0, Lr0, Llo, Lhi, Ld, Lz, Lbo, Lbn, Lfl, Lks, Lgi, La, Lden, Lp, Lx2, Lzz, Lm,
+                                 coef, false);
     }
     t1 = __builtin_amdgcn_s_memtime() - tr;
   }
@@ -112,19 +119,28 @@ void run(int bs, int nact) {
   hipMemset(sc, 0, sizeof(Scal));
   d.sc = sc;
   const size_t lds = 8 * (size_t)B * B + 8 * (size_t)B * 18 + 4 * (size_t)B * 4;
-  hipFuncSetAttribute((const void *)k_mb_br<B>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipFuncSetAttribute((const void *)k_mb_br<B, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipFuncSetAttribute((const void *)k_mb_br<B, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int reps = 200;
-  for (int pass = 0; pass < 2; ++pass) {
-    hipLaunchKernelGGL(k_mb_br<B>, dim3(1), dim3(512), lds, 0, d, dG, dgi, dr0, dD, dz, dbo, dfl, dbn, dc, reps, bs);
-    hipDeviceSynchronize();
+  std::vector<double> bn0(B);
+  for (int v = 0; v < 2; ++v) {
+    for (int pass = 0; pass < 2; ++pass) {
+      if (v == 0) hipLaunchKernelGGL((k_mb_br<B, 0>), dim3(1), dim3(512), lds, 0, d, dG, dgi, dr0, dD, dz, dbo, dfl, dbn, dc, reps, bs);
+      else hipLaunchKernelGGL((k_mb_br<B, 1>), dim3(1), dim3(512), lds, 0, d, dG, dgi, dr0, dD, dz, dbo, dfl, dbn, dc, reps, bs);
+      hipDeviceSynchronize();
+    }
+    unsigned long long c = 0;
+    hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
+    hipMemcpy(bn.data(), dbn, 8 * B, hipMemcpyDeviceToHost);
+    double err = 0;
+    for (int j = 0; j < bs; ++j) err = fmax(err, fabs(bn[j] - ref[j]) / fmax(1e-300, fabs(ref[j])));
+    int same = 1;
+    if (v == 0) bn0 = bn;
+    else for (int j = 0; j < bs; ++j) same &= std::memcmp(&bn[j], &bn0[j], 8) == 0;
+    std::printf("BayesR resident chain %-9s B=%d bs=%d act=%d: %.1f cycles/step (%.0f cycles/block), max rel err %.2e%s\n",
+                v ? "sub-block" : "per-step", B, bs, nact, (double)c / ((double)reps * nact), (double)c / reps, err,
+                v ? (same ? ", bit-identical to per-step" : ", DIFFERS from per-step") : "");
   }
-  unsigned long long c = 0;
-  hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
-  hipMemcpy(bn.data(), dbn, 8 * B, hipMemcpyDeviceToHost);
-  double err = 0;
-  for (int j = 0; j < bs; ++j) err = fmax(err, fabs(bn[j] - ref[j]) / fmax(1e-300, fabs(ref[j])));
-  std::printf("BayesR resident chain B=%d bs=%d act=%d: %.1f cycles/step (%.0f cycles/block), max rel err %.2e\n", B,
-              bs, nact, (double)c / ((double)reps * nact), (double)c / reps, err);
 }
 
 int main() {
