@@ -21,8 +21,9 @@ tail -1 gpurun_out/${TAG}_trace.log | cut -c1-300; }
 if [ -n "$ALG" ]; then
   for c in FETCH_SIZE WRITE_SIZE; do
     # counter collection serialises dispatches: the two side-by-side kernels of the default sweep
-    # cannot be co-resident under it, so the PMC passes count the one-kernel form of the same
-    # roles (BRR_FUSED_SINGLE=1)
+    # cannot be co-resident under it, so the PMC passes count the one-kernel form of the same roles
+    # (BRR_FUSED_SINGLE=1), which since round 5 instantiates the timed form's streaming variant: the
+    # f32 list prefetch (C2) and the class-code cache (C4: k_sweep<true, 128, 2>)
     BRR_FUSED_SINGLE=1 timeout -k 10 -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex 'k_sweep' -d gpurun_out/${TAG}_pmc_$c -o pmc \
       --output-format csv -- python3 bench.py --steps 2 --warmup 10 --no-roofline-events $ARGS \
       > gpurun_out/${TAG}_pmc_$c.log 2>&1 || { echo "PMC $c FAILED"; tail -20 gpurun_out/${TAG}_pmc_$c.log; exit 1; }
