@@ -1365,6 +1365,86 @@ __device__ __forceinline__ FastDec decide_fast(double r, const double *a, const 
   return o;
 }
 
+// decide_fast for ONE position, evaluated by a whole wave with every lane active (the serial chains'
+// re-decision, wave-uniform arguments): component k on lane k, so the K exponentials and the K quotients
+// of the softmax issue once, side by side, instead of K times on the chain.  Every element is the same
+// operation on the same values as in decide_fast and every sum runs in the same order (maxima and minima
+// are exact in any order): the result is bit-identical to decide_fast's.
+__device__ __forceinline__ FastDec decide_fast_wave(double r, const double *a, const double *den, int64_t stride, int K,
+                                                    double sigmaE, double p) {
+#pragma clang fp contract(off)
+  FastDec o;
+  o.ex = false;
+  const double t = r * r;
+  if (K == 1) { o.k = 0; o.lo = -1e308; o.hi = 1e308; return o; }
+  const int lane = threadIdx.x & 63;
+  const int kl = lane < K ? lane : 0;  // this lane's component
+  const double dk = den[(max(kl, 1) - 1) * stride];  // (read for every lane: no divergent load)
+  const double sl = kl == 0 ? 0.0 : 0.5 / (dk * sigmaE);
+  const double Lk = a[kl * stride] + sl * t;
+  double mx = -1e308, mn = 1e308, smax = 0.0;
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) {
+    if (k < K) {
+      const double v = readlane_f64(Lk, k);
+      mx = fmax(mx, v);
+      mn = fmin(mn, v);
+      smax = fmax(smax, readlane_f64(sl, k));
+    }
+  }
+  if (!(mx - mn < 690.0) || !(smax > 0.0)) { o.ex = true; o.k = 0; o.lo = 1.0; o.hi = -1.0; return o; }
+  const double ek = exp(Lk - mx);
+  double S = 0.0, ev[MAXK];
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) {
+    if (k < K) { ev[k] = readlane_f64(ek, k); S += ev[k]; }
+  }
+  double acc = 0.0, myacc = 0.0;
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) {
+    if (k < K) {
+      acc += ev[k];
+      myacc = kl == k ? acc : myacc;
+    }
+  }
+  const double Ak = myacc / S;  // lane k: A[k]
+  int sel = FALLTHROUGH;
+  double Asel = 0.0, Aprev = 0.0, Al = 0.0;
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) {
+    if (k < K) {
+      const double A = readlane_f64(Ak, k);
+      if (sel == FALLTHROUGH && p <= A) { sel = k; Asel = A; Aprev = Al; }
+      Al = A;
+    }
+  }
+  const double E = 2.718281828459045;
+  // the two side widths and 1 / smax on lanes 0, 1, 2
+  const double gap = lane == 0 ? Asel - p : p - Aprev;
+  const double Ag = lane == 0 ? Asel : Aprev;
+  double sw;
+  if (!(gap > 1e-12)) sw = 0.0;
+  else {
+    const double m = fmin(Ag, 1.0 - Ag);
+    sw = m > 0.0 ? gap / (E * smax * m) : 1e300;
+  }
+  const double ism = 1.0 / smax;
+  double w;
+  if (sel == FALLTHROUGH) {
+    w = 0.0;  // p above the last cumulative sum: only the exact formula decides
+  } else {
+    w = readlane_f64(sw, 0);
+    if (sel > 0) w = fmin(w, readlane_f64(sw, 1));
+  }
+  w = fmin(w, ism);
+  const double mg = 0.5 * w;
+  o.k = sel;
+  if (!(mg > 0.0)) { o.ex = true; o.lo = 1.0; o.hi = -1.0; return o; }
+  o.lo = t - mg;
+  o.hi = t + mg;
+  return o;
+}
+
 // Decision with the window, exact fallback included (parallel phases: prep and refresh).
 __device__ __forceinline__ FastDec decide_pos(const Dev &d, double r, const double *a, const double *den, int64_t stride,
                                               double sigmaE, double p, double x2, int m) {
@@ -1391,12 +1471,13 @@ __device__ __noinline__ Decision decide_bayesr_ool(double num, double xsq, doubl
                                                    bool want_margin) {
   return decide_bayesr(num, xsq, sigmaE, sigmaG, pi_g, cva_g, Gs, K, p, want_margin);
 }
-// decide_pos for the chains: the fast decision inline, the exact fallback out of line
+// decide_pos for the chains (a whole wave, uniform arguments): the fast decision inline and spread over the
+// K lanes, the exact fallback out of line
 __device__ __forceinline__ FastDec decide_pos_ool(const int *gAssign, const double *sigmaGG, const double *pi,
                                                   const double *cva, int G, int K, double r, const double *a,
                                                   const double *den, int64_t stride, double sigmaE, double p,
                                                   double x2, int m) {
-  FastDec o = decide_fast(r, a, den, stride, K, sigmaE, p);
+  FastDec o = decide_fast_wave(r, a, den, stride, K, sigmaE, p);
   if (o.ex) {
     const int g = gAssign ? gAssign[m] : 0;
     Decision dc = decide_bayesr_ool(r, x2, sigmaE, sigmaGG[g], pi + (int64_t)g * K, cva + g, G, K, p, true);
@@ -3778,6 +3859,13 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
   const int lag = sweep_lag(d);
   double *s_ld = s_red + RED_NT;                            // a change list: deltas [B + 16]
   int *s_lg = reinterpret_cast<int *>(s_ld + (B + 16));     // and Gram indices [B + 16]
+  // the cross-Gram block of block sp's changes against block s (l = s - 1 - sp)
+  auto xblock = [&](int l, int sp, int s) -> const double * {
+    const int gp = d.gblk[sp], gb = d.gblk[s];
+    return l == 0 ? (gb == (gp + 1) % d.nb ? d.xgram + (int64_t)gp * B * B : d.xgramT + (int64_t)gb * B * B)
+         : l == 1 ? (gb == (gp + 2) % d.nb ? d.xgram2 + (int64_t)gp * B * B : d.xgram2T + (int64_t)gb * B * B)
+                  : (gb == (gp + 3) % d.nb ? d.xgram3 + (int64_t)gp * B * B : d.xgram3T + (int64_t)gb * B * B);
+  };
   for (int s = d.seg0; s < d.seg1; ++s) {
     const int par = s % NPAR;
     const int use = d.gbase[par] + s / NPAR;
@@ -3805,7 +3893,7 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
       for (int p = 1; p < np; ++p) tot += s_red[p * cw + t];
     }
     if (d.rcorr && s > d.seg0) {
-      const int bs = d.bsz[s], gb = d.gblk[s];
+      const int bs = d.bsz[s];
       // the column's Gram index (slab columns are visit positions, or storage indices = Gram indices)
       const int gic = col < bs ? (d.slab_storage ? col : d.gidx[(int64_t)s * B + col]) : 0;
       double cor[LAG_MAX] = {0.0, 0.0, 0.0};
@@ -3823,14 +3911,11 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
           s_ld[e] = ld_sc1(pbn + e) - ld_sc1(pbo + e);
         }
         __syncthreads();
-        const int gp = d.gblk[sp];
-        const double *C = l == 0 ? (gb == (gp + 1) % d.nb ? d.xgram + (int64_t)gp * B * B : d.xgramT + (int64_t)gb * B * B)
-                        : l == 1 ? (gb == (gp + 2) % d.nb ? d.xgram2 + (int64_t)gp * B * B : d.xgram2T + (int64_t)gb * B * B)
-                                 : (gb == (gp + 3) % d.nb ? d.xgram3 + (int64_t)gp * B * B : d.xgram3T + (int64_t)gb * B * B);
         if (t < RED_NT) {
           const int e0 = part * nr / np, e1 = (part + 1) * nr / np;
           double a = 0.0;
           if (col < bs) {
+            const double *C = xblock(l, sp, s);
             for (int e = e0; e < e1; e += 8) {
               double v[8];
 #pragma unroll

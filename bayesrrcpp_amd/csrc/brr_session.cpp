@@ -1239,11 +1239,13 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     // finds every column class-coded, and where LDS holds lag + 2 blocks of them) and apply the
     // change lists from them instead of re-reading X -- on by default for the Horseshoe, whose
     // lists hold every column of a block (C4 13.05 -> 14.1 sweeps/s with the round-4 apply tables
-    // and reducers, profiles/r04i_ab.log; round 3: 13.87 -> 13.42); the other samplers' lists are
-    // short (C2, C3: no change).  BRR_F32_CODE_CACHE=0|1 overrides.
+    // and reducers, profiles/r04i_ab.log; round 3: 13.87 -> 13.42), and for Groups (C3 12.24 -> 12.28
+    // sweeps/s, same box, profiles/r05e_ab.log: no slower, and the apply no longer re-reads the changed
+    // columns, 1.30x -> ~1.0x the algorithmic bytes); V2 / restart change few markers per block (C2: no
+    // change).  BRR_F32_CODE_CACHE=0|1 overrides.
     const char *fcc = getenv("BRR_F32_CODE_CACHE");
     const bool f32cc = !s->x2bit && s->order_mode == BRR_ORDER_BLOCKED &&
-                       (fcc ? fcc[0] == '1' : model == MODEL_HORSESHOE);
+                       (fcc ? fcc[0] == '1' : (model == MODEL_HORSESHOE || model == MODEL_GROUPS));
     if (rows || ref2bit || (pb && pb[0] == '1') || !fused_config(d, cus, cap ? atoi(cap) : 0, &s->fused, f32cc))
       s->fused = FusedCfg{};
     if (s->fused.nsg == 0) d.lag = 1;
