@@ -233,7 +233,7 @@ def test_2bit_code_cache_midsize(brr, require_gpu, monkeypatch, model, cap):
 @pytest.mark.parametrize("model", [1, 3])
 def test_f32_class_code_cache_identical(brr, oracle_mod, require_gpu, model, monkeypatch):
     """f32 storage with every column class-coded (BLOCKED order, B = 128, BRR_F32_CODE_CACHE=1; the
-    Horseshoe's default): the streamers keep the streamed blocks' class codes in LDS and apply the
+    Horseshoe's and, since round 5, the Groups model's default): the streamers keep the streamed blocks' class codes in LDS and apply the
     change lists from them (k_sweep_stream<2>) instead of re-reading X.  Same values in the same
     order: the chain equals the f32 chain without the cache (BRR_F32_CODE_CACHE=0) bit for bit, and
     the oracle within the parity tolerance."""
@@ -251,7 +251,7 @@ def test_f32_class_code_cache_identical(brr, oracle_mod, require_gpu, model, mon
     assert b.scalar(105) == 0
     monkeypatch.delenv("BRR_F32_CODE_CACHE")
     dflt = _session(brr, L, model, X, Y, 128, L.X_F32, G, gA)
-    assert dflt.scalar(105) == (1 if model == L.MODEL_HORSESHOE else 0), "the Horseshoe's default is the cache"
+    assert dflt.scalar(105) == 1, "the cache is the default of the Horseshoe and Groups models"
     del dflt
     for it in range(4):
         a.sweep(1)
