@@ -2976,7 +2976,13 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     }
     if (t == 0) misc[12] = s + 1;
   }
-  // 4) write back, compact the changed markers into this block's list (position order)
+  // 4) write back, compact the changed markers into this block's list in Gram-index (storage) order: a
+  //    list holding every position (the Horseshoe's) is then the block's columns in storage order, which
+  //    the streamers' apply reads 16 at a time from their code tiles (apply_pending); every consumer
+  //    (apply, cross-Gram corrections) sums a list in list order
+  int *Lpg = Lspos;  // the position of each Gram index (the chain's prediction list is no longer read)
+  for (int pos = t; pos < bs; pos += NT) Lpg[Lgi[pos]] = pos;
+  __syncthreads();
   const int pslot = s % NSLOT;
   int *pidx = d.pend_idx + pslot * d.pend_stride, *pgi = d.pend_gi + pslot * d.pend_stride;
   int *ppos = d.pend_pos + pslot * d.pend_stride;
@@ -2984,11 +2990,12 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
   base = 0;
 #pragma unroll
   for (int c = 0; c < NPT; ++c) {
-    const int pos = t + NT * c;
+    const int gi = t + NT * c;  // (Lgi is a permutation of 0 .. bs - 1)
+    const int pos = gi < bs ? Lpg[gi] : 0;
     int changed = 0;
     double bnv = 0.0, bov = 0.0;
     int m = 0;
-    if (pos < bs) {
+    if (gi < bs) {
       m = Lm[pos];
       bnv = Lbn[pos];
       bov = Lbo[pos];
@@ -3002,13 +3009,13 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
     if (changed) {
       const int idx = pre + __popcll(bal & ((1ull << lane) - 1ull));
       st_sc1_int(pidx + idx, m);
-      st_sc1_int(pgi + idx, Lgi[pos]);
+      st_sc1_int(pgi + idx, gi);
       st_sc1_int(ppos + idx, pos);
       st_sc1(pbo + idx, bov);
       st_sc1(pbn + idx, bnv);
       if (nlb > 0) {  // the next blocks' cross-Gram corrections read it from LDS (phase A)
         Llist[(int64_t)(s % nlb) * (B + 16) + idx] = bnv - bov;
-        Lligi[(int64_t)(s % nlb) * (B + 16) + idx] = Lgi[pos];
+        Lligi[(int64_t)(s % nlb) * (B + 16) + idx] = gi;
       }
     }
     for (int w = 0; w < NW; ++w) base += misc[w];
@@ -3156,9 +3163,20 @@ constexpr int FUSED_GROUP = FUSED_GROUP_N;
 // workgroup's extra waves take whole passes of one-part lists or sit a long list out, so a residual
 // row sees the same operations in the same order under every streamer geometry.)
 constexpr int APPLY_NW = 8;
-__device__ __forceinline__ int apply_nparts(int np, int npass) {
-  return (npass >= APPLY_NW || np <= BRR_APPLY_SMALL) ? 1 : APPLY_NW / npass;
+// Uniform integer division by a small run-time divisor in the apply: a scalar loop (the compiler's
+// expansion goes through a VALU reciprocal whose loop-invariant constants it hoists into VGPRs).
+__device__ __forceinline__ int small_div(int x, int d, int *rem) {  // x >= 0, d >= 1 uniform, x / d small
+  int q = 0;
+  while (x >= d) { x -= d; ++q; }
+  *rem = x;
+  return q;
 }
+__device__ __forceinline__ int apply_nparts(int np, int npass) {
+  int r;
+  return (npass >= APPLY_NW || np <= BRR_APPLY_SMALL) ? 1 : small_div(APPLY_NW, npass, &r);
+}
+// (G = 8 / npass is 8, 4, 2 or 1: the part bounds np part / G are shifts)
+__device__ __forceinline__ int part_bound(int np, int part, int G) { return (np * part) >> (31 - __builtin_clz(G)); }
 template <int XF, int NT = SWEEP_NT>
 __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0, int64_t r1, int npass,
                                               double *eps_l, int *s_pidx, double *s_pbo, double *s_pbn,
@@ -3205,11 +3223,6 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
         if (XF) {
           s_ppos[lane] = gi0;
           s_cb[lane] = ccode ? (int64_t)(gi0 >> 4) * (npass * 64 * 16) + (gi0 & 15) : code_off(col0, 0, d.B, d.ldc);
-          // the entry's value x delta table: the residual update adds W[code] per row, the product the
-          // f32 path forms as x * (b_old - b_new) (the same rounded product, then the same add)
-          const double *lt = lutb + 4 * gi0;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) s_w[4 * lane + k] = lt[k] * pd0;
         }
         s_pd[lane] = pd0;
       }
@@ -3225,24 +3238,52 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
         const int gi = ld_sc1_int(d.pend_gi + slot * d.pend_stride + es);  // in-block (storage) index
         s_ppos[e] = gi;
         s_cb[e] = ccode ? (int64_t)(gi >> 4) * (npass * 64 * 16) + (gi & 15) : code_off(col, 0, d.B, d.ldc);
-        const double *lt = lutb + 4 * gi;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s_w[4 * e + k] = lt[k] * pde;
       }
       s_pd[e] = pde;
     }
-    if (lane == 0) { s_np[0] = np; s_np[1] = nr; }
+    if (XF) {
+      // the pair tables: entries 2q and 2q + 1 add W[c0 | c1 << 2] = (x0(c0) d0) + (x1(c1) d1) per row,
+      // the f32 path's (x0 d0 + x1 d1) (the same rounded products, then the same adds); an entry
+      // without a real partner (2q + 1 >= nr) adds x0(c0) d0 alone, as the f32 path does.  (This
+      // wave's LDS writes above are visible to its own reads below: LDS operations of a wave complete
+      // in order.)
+      for (int q = lane; 2 * q < np; q += 64) {
+        const int e = 2 * q;
+        const double *l0 = lutb + 4 * s_ppos[e], *l1 = lutb + 4 * s_ppos[e + 1];
+        const double d0 = s_pd[e], d1 = s_pd[e + 1];
+        const bool single = e + 1 >= nr;
+        double w0[4], w1[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { w0[k] = l0[k] * d0; w1[k] = l1[k] * d1; }
+        double *wq = s_w + 16 * q;
+#pragma unroll
+        for (int c1 = 0; c1 < 4; ++c1)
+#pragma unroll
+          for (int c0 = 0; c0 < 4; ++c0) wq[c0 + 4 * c1] = single ? w0[c0] : w0[c0] + w1[c1];
+      }
+    }
+    // (table storage) dense: the list is the block's first nr columns in storage order -- the
+    // Horseshoe's every block (the solver writes lists in storage order, solve_block)
+    bool dn = true;
+    if (XF)
+      for (int e = lane; e < nr; e += 64) dn = dn && s_ppos[e] == e;
+    const bool dense_l = XF && __ballot(!dn) == 0;
+    if (lane == 0) { s_np[0] = np; s_np[1] = nr | (dense_l ? 1 << 30 : 0); }
   }
   __syncthreads();
   const int np = __builtin_amdgcn_readfirstlane(s_np[0]);
-  const int nr = __builtin_amdgcn_readfirstlane(s_np[1]);
+  const int nr_d = __builtin_amdgcn_readfirstlane(s_np[1]);
+  const int nr = nr_d & ((1 << 30) - 1);
+  const bool dense = XF && (nr_d >> 30) != 0;
   const uint64_t tq1 = ptime ? wall_clock64() : 0;
   const int G = apply_nparts(np, npass);  // parts of the list
   const int ldp = npass * SROWS;                          // doubles per part in s_part
   if (np > 0) {
-    const int p0 = G == 1 ? w : w % npass, part = G == 1 ? 0 : w / npass;
+    int wr;
+    const int wq = small_div(w, npass, &wr);
+    const int p0 = G == 1 ? w : wr, part = G == 1 ? 0 : wq;
     const int pstep = G == 1 ? NT / 64 : npass;  // (G > 1: one pass per wave)
-    const int e0 = part < G ? (np * part / G) : np, e1 = part < G ? (np * (part + 1) / G) : np;
+    const int e0 = part < G ? part_bound(np, part, G) : np, e1 = part < G ? part_bound(np, part + 1, G) : np;
     // the part's real entries: the neutral padding's products are exact zeros and are skipped
     const int ee = min(e1, nr);
     for (int p = p0; p < npass && e0 < e1; p += pstep) {
@@ -3254,32 +3295,73 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
       };
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
       if constexpr (XF) {
-        // 2-bit: raw code bytes in flight (2 batches of AB), decoded when consumed; the byte of
-        // (entry e, this lane's quad) from LDS or HBM in separate loops (concrete address spaces)
+        // table storage: per pair of entries one LDS read and one add per row (the pair tables).  The
+        // byte of (entry e, this lane's quad) from LDS (code cache) or HBM in separate loops (concrete
+        // address spaces).
+        auto pair_load = [&](uint32_t b0, uint32_t b1, int e, double (&wv)[4]) __attribute__((always_inline)) {
+          const double *wq = s_w + 8 * e;  // (e even: the tables of pair e / 2)
+          const uint32_t m = b0 | (b1 << 8);
+          wv[0] = wq[__builtin_amdgcn_ubfe(m, 0, 2) | (__builtin_amdgcn_ubfe(m, 8, 2) << 2)];
+          wv[1] = wq[__builtin_amdgcn_ubfe(m, 2, 2) | (__builtin_amdgcn_ubfe(m, 10, 2) << 2)];
+          wv[2] = wq[__builtin_amdgcn_ubfe(m, 4, 2) | (__builtin_amdgcn_ubfe(m, 12, 2) << 2)];
+          wv[3] = wq[__builtin_amdgcn_ubfe(m, 6, 2) | (__builtin_amdgcn_ubfe(m, 14, 2) << 2)];
+        };
+        auto pair_add = [&](uint32_t b0, uint32_t b1, int e) __attribute__((always_inline)) {
+          double wv[4];
+          pair_load(b0, b1, e, wv);
+          a0 = a0 + wv[0];
+          a1 = a1 + wv[1];
+          a2 = a2 + wv[2];
+          a3 = a3 + wv[3];
+        };
         auto run = [&](auto lds_c) __attribute__((always_inline)) {
           constexpr bool LDSC = decltype(lds_c)::value;
           const int64_t qo = LDSC ? (int64_t)(off >> 2) * 16 : (src >> 2) * 16;
+          if (e0 >= ee) return;
+          if (dense) {
+            // the list is the block's first nr columns in storage order: entries 16 g .. 16 g + 15 are
+            // one 16-byte code group at this lane's quad (1 read for 16 entries instead of 2 per entry)
+            auto gload = [&](int gq) __attribute__((always_inline)) -> uint4 {
+              if constexpr (LDSC) {
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4 *>(
+                    (const __attribute__((address_space(3))) uint8_t *)ccode + s_cb[16 * gq] + qo);
+                return make_uint4(v.x, v.y, v.z, v.w);
+              } else
+                return *reinterpret_cast<const uint4 *>(d.Xc + s_cb[16 * gq] + qo);
+            };
+            const int g1 = (ee - 1) >> 4;
+            uint4 cur = gload(e0 >> 4);
+            auto byte_of = [&](const uint4 &c, int k) __attribute__((always_inline)) -> uint32_t {  // k static
+              const uint32_t word = k < 4 ? c.x : (k < 8 ? c.y : (k < 12 ? c.z : c.w));
+              return __builtin_amdgcn_ubfe(word, 8 * (k & 3), 8);
+            };
+            for (int gq = e0 >> 4; gq <= g1; ++gq) {
+              const uint4 nxt = gload(min(gq + 1, g1));
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const int e = 16 * gq + 2 * j;
+                if (e >= e0 && e < ee) pair_add(byte_of(cur, 2 * j), byte_of(cur, 2 * j + 1), e);
+              }
+              cur = nxt;
+            }
+            return;
+          }
           auto rload = [&](int e) __attribute__((always_inline)) -> uint32_t {
             if constexpr (LDSC)
               return ((const __attribute__((address_space(3))) uint8_t *)ccode)[s_cb[e] + qo];
             else
               return d.Xc[s_cb[e] + qo];
           };
+          // raw code bytes in flight (2 batches of AB entries, AB even: whole pairs), decoded when
+          // consumed; a pair's second byte past ee is read clamped and not used (its table is the
+          // first entry's alone)
           uint32_t ra[AB], rb[AB];
           auto consume = [&](const uint32_t (&r)[AB], int e) __attribute__((always_inline)) {
 #pragma unroll
-            for (int q = 0; q < AB; ++q) {
-              if (e + q < ee) {
-                const double *w = s_w + 4 * (e + q);  // x delta by code: one LDS read and one add per row
-                const uint32_t b = r[q];
-                a0 = a0 + w[b & 3u];
-                a1 = a1 + w[(b >> 2) & 3u];
-                a2 = a2 + w[(b >> 4) & 3u];
-                a3 = a3 + w[(b >> 6) & 3u];
-              }
-            }
+            for (int q = 0; q < AB; q += 2)
+              if (e + q < ee) pair_add(r[q], r[q + 1], e + q);
           };
-          if (e0 >= ee) return;
 #pragma unroll
           for (int q = 0; q < AB; ++q) ra[q] = rload(min(e0 + q, ee - 1));
           for (int e = e0; e < ee; e += 2 * AB) {
@@ -3303,13 +3385,21 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
       float4 xa[AB], xb[AB];
       auto consume = [&](const float4 (&x)[AB], int e) __attribute__((always_inline)) {
 #pragma unroll
-        for (int q = 0; q < AB; ++q) {
-          if (e + q < ee) {
-            const double dd = s_pd[e + q];  // (rounded product, then the add: the 2-bit path's W[code])
-            a0 = a0 + (double)x[q].x * dd;
-            a1 = a1 + (double)x[q].y * dd;
-            a2 = a2 + (double)x[q].z * dd;
-            a3 = a3 + (double)x[q].w * dd;
+        for (int q = 0; q < AB; q += 2) {
+          // pairs of entries: (x0 d0 + x1 d1) per row, then the add (rounded products: the table
+          // storages' pair tables); an entry without a partner in the part alone
+          if (e + q + 1 < ee) {
+            const double d0 = s_pd[e + q], d1 = s_pd[e + q + 1];
+            a0 = a0 + ((double)x[q].x * d0 + (double)x[q + 1].x * d1);
+            a1 = a1 + ((double)x[q].y * d0 + (double)x[q + 1].y * d1);
+            a2 = a2 + ((double)x[q].z * d0 + (double)x[q + 1].z * d1);
+            a3 = a3 + ((double)x[q].w * d0 + (double)x[q + 1].w * d1);
+          } else if (e + q < ee) {
+            const double d0 = s_pd[e + q];
+            a0 = a0 + (double)x[q].x * d0;
+            a1 = a1 + (double)x[q].y * d0;
+            a2 = a2 + (double)x[q].z * d0;
+            a3 = a3 + (double)x[q].w * d0;
           }
         }
       };
@@ -3352,10 +3442,9 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
     if (ptime) { ptime[0] += tq1 - tq0; ptime[1] += tq2 - tq1; }
     if (G > 1) {
       // parts without a pass (G npass < 8 waves, or an empty part) hold nothing: zero them first
-      for (int i = t; i < G * ldp; i += NT) {
-        const int part = i / ldp;
-        if (np * part / G == np * (part + 1) / G) s_part[i] = 0.0;
-      }
+      for (int pt = 0; pt < G; ++pt)
+        if (part_bound(np, pt, G) == part_bound(np, pt + 1, G))
+          for (int i = t; i < ldp; i += NT) s_part[pt * ldp + i] = 0.0;
       __syncthreads();
       if (ptime) ptime[2] += wall_clock64() - tq2;
       for (int i = t; i < ldp; i += NT) {
@@ -3384,8 +3473,10 @@ struct ApplyPart {
 };
 __device__ __forceinline__ ApplyPart apply_part(int np, int npass, int w) {
   const int G = apply_nparts(np, npass);
-  const int p0 = G == 1 ? w : w % npass, part = G == 1 ? 0 : w / npass;
-  return {p0, part < G ? (np * part / G) : np, part < G ? (np * (part + 1) / G) : np};
+  int wr;
+  const int wq = small_div(w, npass, &wr);
+  const int p0 = G == 1 ? w : wr, part = G == 1 ? 0 : wq;
+  return {p0, part < G ? part_bound(np, part, G) : np, part < G ? part_bound(np, part + 1, G) : np};
 }
 
 // apply_pending for f32 storage when every wave of the workgroup prefetched the list during the
@@ -3408,18 +3499,28 @@ __device__ __forceinline__ void apply_staged(const Dev &d, int np, int nr, doubl
   const int ldp = npass * SROWS;
   if (np > 0) {
     const ApplyPart ap = apply_part(np, npass, w);
-    const int part = G == 1 ? 0 : w / npass;
+    int wr;
+    const int part = G == 1 ? 0 : small_div(w, npass, &wr);
     if (ap.p0 < npass && ap.e0 < ap.e1) {
       const int off = ap.p0 * SROWS + 4 * lane;
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
       const int ee = min(ap.e1, nr);
-      for (int e = ap.e0; e < ee; ++e) {
-        const double dd = readlane_f64(lpd, e);
+      for (int e = ap.e0; e < ee; e += 2) {  // pairs of entries, as apply_pending
+        const double d0 = readlane_f64(lpd, e);
         const float4 x = *reinterpret_cast<const float4 *>(stage + ((int64_t)e * npass + ap.p0) * SROWS + 4 * lane);
-        a0 = a0 + (double)x.x * dd;
-        a1 = a1 + (double)x.y * dd;
-        a2 = a2 + (double)x.z * dd;
-        a3 = a3 + (double)x.w * dd;
+        if (e + 1 < ee) {
+          const double d1 = readlane_f64(lpd, e + 1);
+          const float4 y = *reinterpret_cast<const float4 *>(stage + ((int64_t)(e + 1) * npass + ap.p0) * SROWS + 4 * lane);
+          a0 = a0 + ((double)x.x * d0 + (double)y.x * d1);
+          a1 = a1 + ((double)x.y * d0 + (double)y.y * d1);
+          a2 = a2 + ((double)x.z * d0 + (double)y.z * d1);
+          a3 = a3 + ((double)x.w * d0 + (double)y.w * d1);
+        } else {
+          a0 = a0 + (double)x.x * d0;
+          a1 = a1 + (double)x.y * d0;
+          a2 = a2 + (double)x.z * d0;
+          a3 = a3 + (double)x.w * d0;
+        }
       }
       if (G == 1) {
         if (r0 + off < r1) {
@@ -3440,10 +3541,9 @@ __device__ __forceinline__ void apply_staged(const Dev &d, int np, int nr, doubl
     const uint64_t tq2 = ptime ? wall_clock64() : 0;
     if (ptime) ptime[1] += tq2 - tq0;
     if (G > 1) {
-      for (int i = t; i < G * ldp; i += SWEEP_NT) {
-        const int pt = i / ldp;
-        if (np * pt / G == np * (pt + 1) / G) s_part[i] = 0.0;
-      }
+      for (int pt = 0; pt < G; ++pt)
+        if (part_bound(np, pt, G) == part_bound(np, pt + 1, G))
+          for (int i = t; i < ldp; i += SWEEP_NT) s_part[pt * ldp + i] = 0.0;
       __syncthreads();
       if (ptime) ptime[2] += wall_clock64() - tq2;
       for (int i = t; i < ldp; i += SWEEP_NT) {
@@ -3468,7 +3568,7 @@ __device__ __forceinline__ void apply_staged(const Dev &d, int np, int nr, doubl
 // Dev::slab_storage).  The value tables of the block being consumed are staged in LDS in storage
 // order (s_lut, B entries) at each block boundary, after the previous block's last item and
 // before the barrier that precedes the first item of the block.
-template <int CW, int P, int XF, int NT = SWEEP_NT>
+template <int CW, int P, int XF, int NT = SWEEP_NT, bool PROF = false>
 __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int npass, double *eps_l, int *s_pidx,
                                             double *s_pbo, double *s_pbn, int *s_np, double *s_lut, int *s_mem,
                                             double *s_part, uint8_t *s_codes, int pfe = 0, int *s_pf = nullptr,
@@ -3480,7 +3580,9 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   const int64_t r0 = (int64_t)g * rpw, r1 = min((int64_t)d.N, r0 + rpw);
   const int B = d.B, nb = d.nb;
   const int64_t ld = d.ld;
-  const bool prof = d.sc->prof_on;
+  // (the diagnostics' timers in a variant of their own: their registers cost the timed variant 46
+  // spilled VGPRs at XF = 2, whose reloads in the apply wait for the whole prefetch ring)
+  const bool prof = PROF && d.sc->prof_on;
   // 2-bit storage: the value tables of blocks s - 2 .. s + 1 in LDS (buffer s & 3): block s + 1's
   // are staged at boundary s (inside the apply), block s - 2's serve the apply
   const int LAG = sweep_lag(d);  // (buffer counts below are within the layout's d.lag)
@@ -3507,6 +3609,14 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   for (int i = t; i < npass * SROWS; i += NT) eps_l[i] = r0 + i < r1 ? d.eps[r0 + i] : 0.0;
   stage_lut(sb0);
   if (sb0 + 1 < sb1) stage_lut(sb0 + 1);
+  // (table storage) the storage block of block s in LDS (s_gb[s & 7]), written by thread 0 P blocks ahead
+  // (at boundary s - P, before its barriers; an item is issued at most P items -- blocks -- ahead): an
+  // item's loads then need no global load first.  (Read from HBM in issue(), that load's wait -- vmcnt
+  // counts in issue order -- drained every load in flight before each item: no prefetch at all.)
+  static_assert(P <= 6, "s_gb holds blocks s .. s + P");
+  __shared__ int s_gb[8];
+  if (XF && t == 0)
+    for (int k = 0; k <= P && sb0 + k < sb1; ++k) s_gb[(sb0 + k) & 7] = d.gblk[sb0 + k];
   // f32 path: the member (column) indices of blocks s and s + 1 live in LDS (s_mem[(s & 1) B ..]),
   // so an item's loads need no scalar-cache miss first; block s + 1's are copied at boundary s
   if constexpr (!XF)
@@ -3542,7 +3652,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       // storage order, as the 2-bit path: the block's 16 contiguous columns of this chunk (clamped
       // to the last column in a short last block: those dots are never read) and their codes
       static_assert(CW == 16, "an item is one 16-column code group");
-      const int64_t gb = d.gblk[s];  // wave-uniform
+      const int64_t gb = __builtin_amdgcn_readfirstlane(s_gb[s & 7]);  // wave-uniform
       const int64_t c0 = gb * B + w * CPW + c * CW;
 #pragma unroll
       for (int j = 0; j < CW; ++j) x[j] = ldg4_stream(d.X + min(c0 + j, d.M - 1) * ld + off);
@@ -3550,7 +3660,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
       x[CW] = make_float4(__uint_as_float(cg.x), __uint_as_float(cg.y), __uint_as_float(cg.z), __uint_as_float(cg.w));
     } else if constexpr (XF) {
       static_assert(CW == 16, "a 2-bit item is one 16-column group");
-      const int64_t gb = d.gblk[s];  // wave-uniform
+      const int64_t gb = __builtin_amdgcn_readfirstlane(s_gb[s & 7]);  // wave-uniform
       const int64_t grp = gb * (B >> 4) + ((w * CPW + c * CW) >> 4);
       x[0] = ldg16_stream(d.Xc + (grp * d.ldc + (off >> 2)) * 16);
     } else {
@@ -3628,6 +3738,8 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   };
   auto boundary = [&](int s) __attribute__((always_inline)) {
     const int sr = s - sb0;  // position in this launch
+    // (every boundary past the first has a barrier before block s's items: see s_gb)
+    if (XF && sr >= 1 && t == 0 && s + P < sb1) s_gb[(s + P) & 7] = d.gblk[s + P];
     if (sr >= 1 && sr <= LAG) {
       // a boundary without a change list to apply yet: stage block s+1's tables / indices
       if constexpr (XF) {
@@ -3859,6 +3971,12 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
   const int lag = sweep_lag(d);
   double *s_ld = s_red + RED_NT;                            // a change list: deltas [B + 16]
   int *s_lg = reinterpret_cast<int *>(s_ld + (B + 16));     // and Gram indices [B + 16]
+  // (Dev::rcpf) this reducer's columns of the cross-Gram blocks of the lists block s's dots have not seen,
+  // [list l][row][cw]: their rows (the earlier block's Gram indices) and columns are known before those
+  // lists are published (the visit order is), so they are loaded before the wait -- after the publication
+  // only the list itself is read.  For the Horseshoe (every marker changes: the whole B x B block) this
+  // takes the correction's 128 KB per block off the solver's phase A.
+  double *s_C = reinterpret_cast<double *>(s_lg + (B + 16));
   // the cross-Gram block of block sp's changes against block s (l = s - 1 - sp)
   auto xblock = [&](int l, int sp, int s) -> const double * {
     const int gp = d.gblk[sp], gb = d.gblk[s];
@@ -3870,6 +3988,17 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
     const int par = s % NPAR;
     const int use = d.gbase[par] + s / NPAR;
     const double *slab1 = d.slab1 + par * d.slab1_stride + col;
+    if (d.rcpf && d.rcorr && s > d.seg0 && t < RED_NT) {
+      const int bs = d.bsz[s];
+      const int gic = col < bs ? (d.slab_storage ? col : d.gidx[(int64_t)s * B + col]) : 0;
+      for (int l = 0; l < lag; ++l) {
+        const int sp = s - 1 - l;
+        if (sp < d.seg0) break;
+        const int bsp = d.bsz[sp];  // (rows of a short earlier block past its size are never read)
+        const double *C = xblock(l, sp, s);
+        for (int row = part; row < bsp; row += np) s_C[((int64_t)l * B + row) * cw + cl] = C[(int64_t)row * B + gic];
+      }
+    }
     if (t == 0)
       for (int grp = 0; grp < d.ngr; ++grp)
         wait_geq(d.cnt1 + par * d.ngr + grp, (use + 1) * min(FUSED_GROUP, nsg - grp * FUSED_GROUP), d.sync, 6);
@@ -3915,14 +4044,26 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
           const int e0 = part * nr / np, e1 = (part + 1) * nr / np;
           double a = 0.0;
           if (col < bs) {
-            const double *C = xblock(l, sp, s);
-            for (int e = e0; e < e1; e += 8) {
-              double v[8];
+            if (d.rcpf) {  // the slice in LDS (the same values, summed in the same order)
+              const double *Cs = s_C + (int64_t)l * B * cw + cl;
+              for (int e = e0; e < e1; e += 8) {
+                double v[8];
 #pragma unroll
-              for (int u = 0; u < 8; ++u) v[u] = e + u < e1 ? C[(int64_t)s_lg[e + u] * B + gic] : 0.0;
+                for (int u = 0; u < 8; ++u) v[u] = e + u < e1 ? Cs[(int64_t)s_lg[e + u] * cw] : 0.0;
 #pragma unroll
-              for (int u = 0; u < 8; ++u)
-                if (e + u < e1) a += v[u] * s_ld[e + u];
+                for (int u = 0; u < 8; ++u)
+                  if (e + u < e1) a += v[u] * s_ld[e + u];
+              }
+            } else {
+              const double *C = xblock(l, sp, s);
+              for (int e = e0; e < e1; e += 8) {
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = e + u < e1 ? C[(int64_t)s_lg[e + u] * B + gic] : 0.0;
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                  if (e + u < e1) a += v[u] * s_ld[e + u];
+              }
             }
           }
           s_red[part * cw + cl] = a;
@@ -3994,9 +4135,9 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
     // (2-bit storage: s_mem holds the change positions instead); the apply's partial sums; then
     // the code cache
     double *s_part = reinterpret_cast<double *>(s_mem + 2 * d.B);
-    // (table storage) the apply's value x delta tables, then the code cache
+    // (table storage) the apply's pair tables (16 doubles per pair of list entries), then the code cache
     double *s_w = XF ? s_part + SWEEP_NW * SROWS : nullptr;
-    uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_w + (int64_t)(d.B + 16) * 4) : nullptr;
+    uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_w + (int64_t)(d.B + 16) * 8) : nullptr;
     // (f32 storage) the list prefetch's staging area: pfe entries x npass passes x 1 KiB
     float *s_stage = reinterpret_cast<float *>(s_part + SWEEP_NW * SROWS);
     stream_role<STREAM_CW, XF == 1 ? STREAM_P2 : STREAM_P, XF>(d, (int)blockIdx.x - 1, rpw, npass, eps_l, s_pidx, s_pbo,
@@ -4035,7 +4176,7 @@ __global__ __launch_bounds__(SOLVE_NT, 1) void k_sweep_solve(Dev d, uint32_t it,
 // NT = 1024 (2-bit storage, B >= 256): 16 waves per streaming workgroup at <= 128 VGPRs -- four
 // waves per SIMD instead of two to hide the decode-dot's LDS-read -> FMA latency; every column's
 // partial dot and every residual update are the same operations in the same order as at NT = 512.
-template <int XF, int NT = SWEEP_NT>
+template <int XF, int NT = SWEEP_NT, bool PROF = false>
 __global__ __launch_bounds__(NT, 1) void k_sweep_stream(Dev d, int nsg, int rpw, int npass, int nred, int ccache,
                                                          int pfe) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -4053,12 +4194,12 @@ __global__ __launch_bounds__(NT, 1) void k_sweep_stream(Dev d, int nsg, int rpw,
   int *s_pidx = reinterpret_cast<int *>(s_pbn + (d.B + 16));
   int *s_mem = s_pidx + (d.B + 16);
   double *s_part = reinterpret_cast<double *>(s_mem + 2 * d.B);
-  // (table storage: 2-bit codes, f32 code cache) the apply's value x delta tables, then the code cache
+  // (table storage: 2-bit codes, f32 code cache) the apply's pair tables, then the code cache
   double *s_w = XF ? s_part + SWEEP_NW * SROWS : nullptr;
-  uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_w + (int64_t)(d.B + 16) * 4) : nullptr;
+  uint8_t *s_codes = (XF && ccache) ? reinterpret_cast<uint8_t *>(s_w + (int64_t)(d.B + 16) * 8) : nullptr;
   // (f32 storage) the list prefetch's staging area: pfe entries x npass passes x 1 KiB
   float *s_stage = reinterpret_cast<float *>(s_part + SWEEP_NW * SROWS);
-  stream_role<STREAM_CW, XF == 1 ? STREAM_P2 : STREAM_P, XF, NT>(d, (int)blockIdx.x, rpw, npass, eps_l, s_pidx, s_pbo,
+  stream_role<STREAM_CW, XF == 1 ? STREAM_P2 : STREAM_P, XF, NT, PROF>(d, (int)blockIdx.x, rpw, npass, eps_l, s_pidx, s_pbo,
                                                            s_pbn, s_np, s_lut, s_mem, s_part, s_codes, XF ? 0 : pfe,
                                                            s_pf, s_stage, s_w);
 }
@@ -4448,10 +4589,15 @@ static const void *solve_kernel(int model, int B) {
 }
 
 // 0: f32 storage, 1: 2-bit codes, 2: f32 storage with the class-code cache (Dev::xcodes); nt: threads
-// per streaming workgroup (1024: 2-bit codes only)
-static const void *stream_kernel(int xf, int nt = SWEEP_NT) {
-  if (xf == 1) return nt == 1024 ? (const void *)k_sweep_stream<1, 1024> : (const void *)k_sweep_stream<1>;
-  return xf == 2 ? (const void *)k_sweep_stream<2> : (const void *)k_sweep_stream<0>;
+// per streaming workgroup (1024: 2-bit codes only); prof: the variant with the diagnostics' timers
+template <bool PROF>
+static const void *stream_kernel_t(int xf, int nt) {
+  if (xf == 1)
+    return nt == 1024 ? (const void *)k_sweep_stream<1, 1024, PROF> : (const void *)k_sweep_stream<1, SWEEP_NT, PROF>;
+  return xf == 2 ? (const void *)k_sweep_stream<2, SWEEP_NT, PROF> : (const void *)k_sweep_stream<0, SWEEP_NT, PROF>;
+}
+static const void *stream_kernel(int xf, int nt = SWEEP_NT, bool prof = false) {
+  return prof ? stream_kernel_t<true>(xf, nt) : stream_kernel_t<false>(xf, nt);
 }
 static int stream_variant(const Dev &d, const FusedCfg &c) { return d.Xc ? 1 : (c.f32cc && d.xcodes) ? 2 : 0; }
 
@@ -4518,7 +4664,7 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
   // new betas), the member indices of two blocks in LDS
   // (f32 storage with a class-code cache: the value tables and code tiles as for 2-bit storage)
   const bool tables = xf || f32cc;
-  const size_t lut_bytes = (size_t)d.B * 32 * (d.lag + 3) + (size_t)(d.B + 16) * 32;  // + the apply's x delta tables
+  const size_t lut_bytes = (size_t)d.B * 32 * (d.lag + 3) + (size_t)(d.B + 16) * 64;  // + the apply's pair tables
   const size_t eps_base = (size_t)npass * SROWS * sizeof(double) + (size_t)(d.B + 16) * (2 * sizeof(double) + sizeof(int)) +
                           2 * sizeof(int) * d.B + (size_t)SWEEP_NW * SROWS * sizeof(double);
   const size_t code_bytes = (size_t)(d.lag + 2) * d.B * npass * 64;
@@ -4542,11 +4688,15 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
   const int xv1 = xf ? 1 : ccache ? 2 : 0;
   if (!split) fn = sweep_kernel(d.model, d.B, xv1);
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)budget) != hipSuccess) return false;
-  if (split && hipFuncSetAttribute(fst, hipFuncAttributeMaxDynamicSharedMemorySize, (int)st_budget) != hipSuccess)
-    return false;
-  if (split && !xf && ccache &&
-      hipFuncSetAttribute(stream_kernel(2), hipFuncAttributeMaxDynamicSharedMemorySize, (int)st_budget) != hipSuccess)
-    return false;
+  for (int pv = 0; pv < 2 && split; ++pv) {  // (both the timed and the diagnostics variant)
+    if (hipFuncSetAttribute(stream_kernel(xf ? 1 : 0, stnt, pv), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)st_budget) != hipSuccess)
+      return false;
+    if (!xf && ccache &&
+        hipFuncSetAttribute(stream_kernel(2, SWEEP_NT, pv), hipFuncAttributeMaxDynamicSharedMemorySize, (int)st_budget) !=
+            hipSuccess)
+      return false;
+  }
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, snt, lds) != hipSuccess || per_cu < 1)
     return false;
@@ -4571,6 +4721,10 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
   cfg->lds = lds;
   cfg->ccache = (xf && ccache) ? 1 : 0;
   cfg->f32cc = (!xf && ccache) ? 1 : 0;
+  // room in a reducer's LDS for its cross-Gram slices (reduce_role, Dev::rcpf): the partial sums, a list,
+  // and d.lag slices of B rows x B / nred columns
+  const size_t red_need = 8 * ((size_t)RED_NT + (size_t)(d.B + 16) + (size_t)(d.B + 16) / 2 + (size_t)d.lag * d.B * (d.B / nred));
+  cfg->rcpf = red_need <= (split ? cfg->st_lds : lds) ? 1 : 0;
   return true;
 }
 
@@ -4589,7 +4743,7 @@ hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipS
     // the streaming kernel on the side stream, released by the same event that precedes the
     // solver on the session stream; the session stream waits for it before the next launch
     const int xv = stream_variant(d, c);
-    const void *fs = solve_kernel(d.model, d.B), *ft = stream_kernel(xv, xv == 1 ? c.stnt : SWEEP_NT);
+    const void *fs = solve_kernel(d.model, d.B), *ft = stream_kernel(xv, xv == 1 ? c.stnt : SWEEP_NT, c.prof != 0);
     if (xv == 2) cc = 1;  // (k_sweep_stream<2> always keeps the cache)
     if (!fs || !ft) return hipErrorInvalidValue;
     int total = nsg + 1 + nred;

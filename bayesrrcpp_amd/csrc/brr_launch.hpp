@@ -43,6 +43,8 @@ struct FusedCfg {
   int split = 0;   // solver and streaming workgroups as two kernels side by side (else one k_sweep)
   int pfe = 0;     // (split, f32 storage) list entries the streamers can prefetch before a boundary (0: off)
   int stnt = 512;  // (split) threads per streaming / reducing workgroup (1024: 2-bit codes at B >= 256)
+  int rcpf = 0;    // a reducer's LDS holds its cross-Gram slices (Dev::rcpf)
+  int prof = 0;    // (split) launch the streaming kernel's diagnostics variant (Scal::prof_on is set)
   size_t lds = 0;     // solver workgroup's dynamic LDS (one kernel: every workgroup's)
   size_t st_lds = 0;  // (split) streaming / reducing workgroups' dynamic LDS
 };

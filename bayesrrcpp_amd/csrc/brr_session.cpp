@@ -181,6 +181,7 @@ struct brr_session {
   int census_failures = 0;  // fused sweeps whose residency census failed (the session then runs per block)
   // timing
   bool timing = false;
+  bool prof_on = false;  // diagnostics timers on (scalar 102): the streaming kernel's diagnostics variant
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   // (start event index, kind: 0 = k_stream, 1 = k_solve, 2 = solver per sweep, >= 3: a marker-loop
@@ -491,17 +492,22 @@ int do_sweep_local(brr_session *s) {
     {
       const char *rc = getenv("BRR_RED_CORR");
       dp.rcorr = rc ? (atoi(rc) != 0) : (s->B <= 128 && s->model != MODEL_HORSESHOE);
+      // the reducers' cross-Gram columns loaded before the lists are published (BRR_RED_PF=0: after)
+      const char *pf = getenv("BRR_RED_PF");
+      dp.rcpf = dp.rcorr && s->fused.rcpf && !(pf && pf[0] == '0');
     }
     dp.slab_storage = d.Xc != nullptr || d.xcodes != nullptr;  // streamers read blocks in storage order (2-bit, f32 code cache)
+    FusedCfg fc = s->fused;
+    fc.prof = s->prof_on ? 1 : 0;  // (the streaming kernel's diagnostics variant only while they are on)
     if (s->timing) {
       const size_t i0 = s->ev_used;
       hipEvent_t e0 = s->ev(), e1 = s->ev();
       HIPCHK(hipEventRecord(e0, s->st));
-      HIPCHK(launch_sweep_fused(dp, it, s->fused, s->st, s->st_side, s->ev_go, s->ev_done));
+      HIPCHK(launch_sweep_fused(dp, it, fc, s->st, s->st_side, s->ev_go, s->ev_done));
       HIPCHK(hipEventRecord(e1, s->st));
       s->ev_pairs.push_back({i0, 3 + (s1 - s0)});
     } else {
-      HIPCHK(launch_sweep_fused(dp, it, s->fused, s->st, s->st_side, s->ev_go, s->ev_done));
+      HIPCHK(launch_sweep_fused(dp, it, fc, s->st, s->st_side, s->ev_go, s->ev_done));
     }
   } else if (s1 > s0) {
     // eps buffers relative to the segment start: k_stream(b) reads ebuf[(b - s0) & 1]
@@ -1882,6 +1888,7 @@ int brr_session_set_scalar(brr_session *s, int32_t which, double v) {
     case BRR_SIGMAG: return h2d(s, s->d.sigmaGG, &v, 1);
     case 102:  // diagnostics: k_solve phase timers on/off (resets the totals)
       sc.prof_on = v != 0.0;
+      s->prof_on = sc.prof_on != 0;
       for (auto &x : sc.prof) x = 0;
       HIPCHK(hipMemsetAsync(s->d.trace, 0, sizeof(unsigned long long) * (16 * (size_t)s->nb + 9216), s->st));
       break;
