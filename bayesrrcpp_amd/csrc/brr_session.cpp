@@ -485,16 +485,22 @@ int do_sweep_local(brr_session *s) {
     dp.NG = s->fused.ngroups;  // (1: the reducers write every column's whole sum)
     dp.gtarget = s->fused.nred;
     dp.ngr = s->fused.narr;
-    // the cross-Gram corrections in the reducers for the BayesR family at B <= 128 (C3 10.42 ->
-    // 10.88 sweeps/s); not for the Horseshoe, whose dense lists put the reducers' gathers on the
-    // solver's critical path (C4 13.06 -> 12.43), nor at B = 512 (sparse lists); BRR_RED_CORR=0|1
-    // overrides (profiles/r04g_ab.log)
+    // the cross-Gram corrections in the reducers (Dev::rcorr), for every fused sweep: at B <= 128 C3
+    // 10.42 -> 10.88 sweeps/s (profiles/r04g_ab.log), the Horseshoe at lag 2 15.2 -> 18.8 (its phase A
+    // loses the 5.6 us correction of a dense list), C2 2-bit at lag 2 45.5 -> 50.7 in the driver's window
+    // (profiles/r05i_ab.log); C2 f32 unchanged in the driver's window (32.1-32.5 ms), its steady marker
+    // loop 30.8 -> 31.1 ms (profiles/r05j_ab.log) -- taken there too, so that both storages sum the
+    // corrections in one association and keep bit-identical chains (the solver's own correction sums
+    // in another: BRR_RED_CORR=0, diagnostics, matches the oracle to the same tolerance but not bit
+    // for bit)
     {
       const char *rc = getenv("BRR_RED_CORR");
-      dp.rcorr = rc ? (atoi(rc) != 0) : (s->B <= 128 && s->model != MODEL_HORSESHOE);
-      // the reducers' cross-Gram columns loaded before the lists are published (BRR_RED_PF=0: after)
+      dp.rcorr = rc ? (atoi(rc) != 0) : true;
+      // the reducers' cross-Gram columns loaded before the lists are published: off by default (C4 at
+      // lag 2 18.8 -> 14.7 sweeps/s, C3 12.45 -> 12.2, C1 / C3 at lag 1 within noise;
+      // profiles/r05i_ab.log, r05g*); BRR_RED_PF=1 turns it on where the slices fit a reducer's LDS
       const char *pf = getenv("BRR_RED_PF");
-      dp.rcpf = dp.rcorr && s->fused.rcpf && !(pf && pf[0] == '0');
+      dp.rcpf = dp.rcorr && s->fused.rcpf && pf && pf[0] == '1';
     }
     dp.slab_storage = d.Xc != nullptr || d.xcodes != nullptr;  // streamers read blocks in storage order (2-bit, f32 code cache)
     FusedCfg fc = s->fused;
@@ -1225,15 +1231,16 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     // lag 2 (fused sweep, BLOCKED order, nb >= 4): the streamers apply block s-3's changes
     // before streaming block s, so a workgroup can run two blocks ahead of the solver and
     // per-block jitter among the streamers is absorbed; costs the cross-Gram blocks of blocks
-    // two apart (2 nb B^2 f64 more, computed once at init) and a second correction in the
-    // solver.  Chosen where the streamers bound the sweep: f32 storage and the samplers that
-    // change few markers per block (V2, restart; C2 26.3 -> 27.2 sweeps/s); the solver-bound
-    // Groups / Horseshoe chains and the 2-bit storage keep lag 1 (lag 2 measured 9 / 25 / 7 %
-    // slower there).  BRR_LAG=1|2 overrides.
+    // two apart (2 nb B^2 f64 more, computed once at init) and a second correction -- in the
+    // reducers where they correct the dots (Dev::rcorr, brr::session_sweep), else in the solver.
+    // Chosen for the samplers that change few markers per block (V2, restart; C2 f32 26.3 -> 27.2
+    // sweeps/s) in either storage, and for the Horseshoe, with the reducers' correction: C4 15.2 ->
+    // 18.8 sweeps/s, C2 2-bit 45.5 -> 50.7 in the driver's window (profiles/r05i_ab.log; with the
+    // correction in the solver lag 2 was 25 / 7 % slower than lag 1 there), and for Groups (C3 12.41 ->
+    // 12.58, profiles/r05j_ab.log).  BRR_LAG=1|2 overrides.
     const char *lg = getenv("BRR_LAG");
     const bool lag2_ok = s->order_mode == BRR_ORDER_BLOCKED && s->nb >= 4;
-    const bool lag2_pref = !s->x2bit && (model == MODEL_V2 || model == MODEL_RESTART);
-    d.lag = (lag2_ok && (lg ? atoi(lg) >= 2 : lag2_pref)) ? 2 : 1;
+    d.lag = (lag2_ok && (lg ? atoi(lg) >= 2 : true)) ? 2 : 1;
     if (d.lag == 2 && lg && atoi(lg) >= 3 && s->nb >= 5) d.lag = 3;  // (diagnostics: BRR_LAG=3)
     // row shards: the per-block kernels (the cross-shard sum of a block's dots sits between its
     // streaming and its solve; the fused sweep's in-kernel hand-over is one device's)
@@ -1272,7 +1279,10 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     {
       const char *ls = getenv("BRR_LAG_SWITCH");
       const double per_block = (ls ? atof(ls) : 15.0) * ((double)N / 1e5);
-      d.lag_thresh = lg ? 1e300 : per_block * s->nb;  // (BRR_LAG: that lag in every sweep)
+      // (BRR_LAG: that lag in every sweep after the first.  The Horseshoe and Groups keep lag 2 from the
+      // second sweep on, the burn-in included: the Horseshoe changes every marker in every sweep, Groups ~25 of 128 per block, both
+      // above the switch, and both gain from lag 2 with the reducers' correction)
+      d.lag_thresh = (lg || model == MODEL_HORSESHOE || model == MODEL_GROUPS) ? 1e300 : per_block * s->nb;
     }
     // The streaming kernel's stream must never share a hardware queue with the session stream: a
     // solver kernel ahead of it in the same queue would wait (bounded, census site 5) for streaming

@@ -218,6 +218,53 @@ def test_horseshoe_block512(brr, oracle_mod, require_gpu, B, xs):
         _compare(s, orc, O, L, L.MODEL_HORSESHOE, tag=f"hs B={B} {xs} it={it}")
 
 
+@pytest.mark.parametrize("xs", ["f32", "2bit"])
+def test_horseshoe_default_pipeline(brr, oracle_mod, require_gpu, monkeypatch, xs):
+    """The Horseshoe's default marker loop: lag 2 in every sweep after the first (the burn-in included) with the
+    cross-Gram corrections in the reducers, many blocks and several streaming workgroups, against
+    the oracle."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    monkeypatch.setenv("BRR_STREAM_WG", "5")
+    N, P, B = 1500, 1100, 128
+    X, Y, _ = _cohort(O, N, P, n_causal=30)
+    A = (1 / np.sqrt(N)) * 150 / (P - 150)
+    hs = dict(A=A, v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0)
+    s, orc = _make(brr, O, L.MODEL_HORSESHOE, X, Y, 0, B=B, hs=hs, xs=xs)
+    assert s.scalar(104) > 0 and s.scalar(106) == 2  # fused sweep, lag-2 pipeline
+    for it in range(4):
+        assert int(s.scalar(108)) == (1 if it == 0 else 2)  # this sweep's lag (the first from init: 1)
+        s.sweep(1)
+        orc.sweep(1)
+        _compare(s, orc, O, L, L.MODEL_HORSESHOE, tag=f"hs default {xs} it={it}")
+    s.close()
+
+
+@pytest.mark.parametrize("model,B,xs", [(0, 512, "f32"), (0, 128, "2bit"), (3, 128, "f32")])
+def test_solver_side_correction_matches_oracle(brr, oracle_mod, require_gpu, monkeypatch, model, B, xs):
+    """The cross-Gram corrections summed by the solver instead of the reducers (BRR_RED_CORR=0; the
+    default corrects in the reducers for every fused sweep) at lag 1 and 2, against the oracle."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    monkeypatch.setenv("BRR_STREAM_WG", "5")
+    monkeypatch.setenv("BRR_RED_CORR", "0")
+    N, P = 1500, 4 * B + 100
+    X, Y, _ = _cohort(O, N, P, n_causal=30)
+    hs = None
+    if model == L.MODEL_HORSESHOE:
+        A = (1 / np.sqrt(N)) * 150 / (P - 150)
+        hs = dict(A=A, v0E=1e-3, s02E=1e-3, vL=1.0, vT=1.0, c2=1.0, vC=10.0, sC=10.0)
+    for lag in ("1", "2"):
+        monkeypatch.setenv("BRR_LAG", lag)
+        s, orc = _make(brr, O, model, X, Y, 0, B=B, hs=hs, xs=xs)
+        assert s.scalar(104) > 0
+        for it in range(3):
+            s.sweep(1)
+            orc.sweep(1)
+            _compare(s, orc, O, L, model, tag=f"solver-side correction lag {lag} it={it}")
+        s.close()
+
+
 def test_groups_fixed_effects(brr, oracle_mod, require_gpu):
     from bayesrrcpp_amd import _lib as L
     O = oracle_mod
@@ -534,7 +581,7 @@ def test_recycled_device_memory(brr, oracle_mod, require_gpu):
 @pytest.mark.parametrize("lag", [1, 2, 3])
 @pytest.mark.parametrize("model", [0, 1, 2, 3])  # V2, Groups, restart, Horseshoe
 def test_pipeline_lag_all_models(brr, oracle_mod, require_gpu, monkeypatch, model, lag, xs):
-    """Every pipeline lag (default: 2 for V2 / restart on f32, 1 otherwise; 3 is opt-in) for the
+    """Every pipeline lag (default: 2 for V2 / restart / Horseshoe, 1 for Groups; 3 is opt-in) for the
     other models, against the oracle: many blocks, several streaming workgroups."""
     from bayesrrcpp_amd import _lib as L
     O = oracle_mod
