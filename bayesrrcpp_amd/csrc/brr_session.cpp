@@ -1269,16 +1269,16 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
       delete s;
       return nullptr;
     }
-    // lag 1 while the solver bounds the sweep: more than ~15 changed markers per block at C2's
-    // 100,000 rows (measured crossover of the burn-in sweeps at B = 512; round 3, after the
-    // streamers' list prefetch and the row chain's typed loads: sweeps 5-24 at 34.01 / 34.14 ms
-    // against 34.14 / 34.27 at 9, 34.26 / 34.12 at 12, 34.23 / 34.12 at 20, 35.2 at 4,
-    // profiles/r03_lagswitch_ab.log), scaled with the rows: a block's streaming time and a change's
-    // solver cost (one Gram-row and cross-Gram-row read each) both grow with B; BRR_LAG_SWITCH
-    // overrides the per-block count at 100,000 rows
+    // lag 1 while the solver bounds the sweep: more than ~30 changed markers per block at C2's
+    // 100,000 rows (the burn-in's first sweeps), scaled with the rows: a block's streaming time and a
+    // change's solver cost both grow with them; BRR_LAG_SWITCH overrides the per-block count at
+    // 100,000 rows.  Round 5, with the corrections in the reducers, the driver's window (sweeps 5-24)
+    // at 8 / 15 / 30 / 60: 32.75 / 32.37 / 31.78 / 31.95 ms per step, C2 2-bit flat
+    // (profiles/r05o_ab.log; round 3, with the corrections in the solver, 15 was the crossover,
+    // profiles/r03_lagswitch_ab.log)
     {
       const char *ls = getenv("BRR_LAG_SWITCH");
-      const double per_block = (ls ? atof(ls) : 15.0) * ((double)N / 1e5);
+      const double per_block = (ls ? atof(ls) : 30.0) * ((double)N / 1e5);
       // (BRR_LAG: that lag in every sweep after the first.  The Horseshoe and Groups keep lag 2 from the
       // second sweep on, the burn-in included: the Horseshoe changes every marker in every sweep, Groups ~25 of 128 per block, both
       // above the switch, and both gain from lag 2 with the reducers' correction)

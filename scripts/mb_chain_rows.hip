@@ -26,6 +26,7 @@ __global__ __launch_bounds__(512, 1) void k_mb_rows(Dev d, const double *G, cons
     Lr0[i] = r0[i]; Llo[i] = 0.0; Lhi[i] = 1e300; Ld[i] = D[i]; Lz[i] = sdz[i]; Linv[i] = 1.0 / D[i]; Lbo[i] = bo[i];
     Lgi[i] = gi[i]; Lfl[i] = fl[i]; Lks[i] = fl[i] & 0xFF; Lm[i] = i; Lp[i] = 0.5; Lx2[i] = D[i]; Lzz[i] = 0.0;
     Lslot[i] = -1;
+    Lbn[i] = bo[i];  // (the chain stores only the visited positions' new betas)
     for (int k = 0; k < 4; ++k) La[k * B + i] = 0.0;
     for (int k = 0; k < 3; ++k) Lden[k * B + i] = D[i];
   }
