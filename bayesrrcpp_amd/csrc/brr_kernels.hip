@@ -3156,6 +3156,9 @@ constexpr int FUSED_GROUP = FUSED_GROUP_N;
 // state's, a few real ones plus padding -- is applied by one wave per pass (no cross-wave sum and
 // its barrier); a longer one in SWEEP_NW / npass parts per pass.  Every path applies a list the same
 // way, so the residual does not depend on the storage or on whether the list was prefetched.
+#ifndef BRR_DENSE_PIPE
+#define BRR_DENSE_PIPE 1  // (class-code cache) the dense apply's whole groups software-pipelined (0: one pair at a time)
+#endif
 #ifndef BRR_APPLY_SMALL
 #define BRR_APPLY_SMALL 16
 #endif
@@ -3338,10 +3341,31 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
             };
             for (int gq = e0 >> 4; gq <= g1; ++gq) {
               const uint4 nxt = gload(min(gq + 1, g1));
+              if (BRR_DENSE_PIPE && XF == 2 && 16 * gq >= e0 && 16 * gq + 16 <= ee) {
+                // a whole group, software-pipelined: pair j + 1's table reads are issued before pair
+                // j's adds (a scheduling barrier keeps them there; without it the reads issue one at
+                // a time under the prefetch ring's register pressure)
+                double wv[4], wn[4];
+                pair_load(byte_of(cur, 0), byte_of(cur, 1), 16 * gq, wv);
 #pragma unroll
-              for (int j = 0; j < 8; ++j) {
-                const int e = 16 * gq + 2 * j;
-                if (e >= e0 && e < ee) pair_add(byte_of(cur, 2 * j), byte_of(cur, 2 * j + 1), e);
+                for (int j = 0; j < 8; ++j) {
+                  if (j + 1 < 8) pair_load(byte_of(cur, 2 * j + 2), byte_of(cur, 2 * j + 3), 16 * gq + 2 * j + 2, wn);
+                  __builtin_amdgcn_sched_barrier(0);
+                  a0 = a0 + wv[0];
+                  a1 = a1 + wv[1];
+                  a2 = a2 + wv[2];
+                  a3 = a3 + wv[3];
+                  if (j + 1 < 8) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) wv[k] = wn[k];
+                  }
+                }
+              } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                  const int e = 16 * gq + 2 * j;
+                  if (e >= e0 && e < ee) pair_add(byte_of(cur, 2 * j), byte_of(cur, 2 * j + 1), e);
+                }
               }
               cur = nxt;
             }
