@@ -715,7 +715,14 @@ __global__ __launch_bounds__(256, NP <= 2 ? 2 : 1) void k_gram_int(Dev d, const 
   __shared__ int s_h[2][GI_T][4], s_M[2][GI_T][4], s_E[2][GI_T][4];
   const int gb = blockIdx.x, gb2 = (gb + shift) % nb;
   const int ntile = B / GI_T;
-  const int ti = blockIdx.y / ntile, tj = blockIdx.y % ntile;
+  int ti = blockIdx.y / ntile, tj = blockIdx.y % ntile;
+  const bool mirror = shift == 0 && GT == nullptr;  // a diagonal block: the tiles on and above its diagonal
+  if (mirror) {
+    int y = blockIdx.y;
+    ti = 0;
+    while (y >= ntile - ti) { y -= ntile - ti; ++ti; }
+    tj = ti + y;
+  }
   const int bs = bsz[gb], bs2 = bsz[gb2];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, wi = wv >> 1, wj = wv & 1;
   const int64_t N = d.N, nq = d.ldc;
@@ -887,6 +894,8 @@ __global__ __launch_bounds__(256, NP <= 2 ? 2 : 1) void k_gram_int(Dev d, const 
     }
     g[(int64_t)ii * B + jj] = v;
     if (gt) gt[(int64_t)jj * B + ii] = v;
+    // (a diagonal block's tile below its diagonal: the mirror -- the same correctly rounded dot products)
+    if (mirror && ti != tj) g[(int64_t)jj * B + ii] = v;
   }
 }
 
@@ -4492,7 +4501,10 @@ static hipError_t launch_gram_int_t(const Dev &d, int shift, double *G, double *
       hipFuncSetAttribute((const void *)k_gram_int<NP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (attr != hipSuccess) return attr;
   const int nt = d.B / GI_T;
-  hipLaunchKernelGGL((k_gram_int<NP>), dim3((unsigned)d.nb, (unsigned)(nt * nt)), dim3(256), lds, st, d, d.gram_codes,
+  // diagonal blocks (shift 0, no transposed copy): the nt (nt + 1) / 2 tiles on and above the diagonal,
+  // each written to both halves (G is exactly symmetric)
+  const int ntiles = (shift == 0 && GT == nullptr) ? nt * (nt + 1) / 2 : nt * nt;
+  hipLaunchKernelGGL((k_gram_int<NP>), dim3((unsigned)d.nb, (unsigned)ntiles), dim3(256), lds, st, d, d.gram_codes,
                      d.member, d.bsz, d.B, d.nb, shift, G, GT);
   return hipGetLastError();
 }
