@@ -105,6 +105,8 @@ struct Dev {
   int ngr;          // (fused sweep) arrival groups of the streaming workgroups: the stride of cnt1
   int rcorr;        // (fused sweep) the reducers subtract the cross-Gram corrections from the dots they
                     // write (reduce_role); the solver's phase A then forms none
+  int rcsplit;      // (rcorr) the solver corrects for the newest list (block s-1: its own, in its LDS) and the
+                    // reducers for the older ones only, so the dots need not wait for the newest publication
   int rcpf;         // (rcorr) the reducers load their columns of those cross-Gram blocks into LDS before the
                     // lists are published
   int slab_storage; // the partial dots are indexed by in-block storage index, not visit position

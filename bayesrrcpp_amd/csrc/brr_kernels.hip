@@ -2595,7 +2595,8 @@ __device__ __forceinline__ void solve_block(const Dev &d, int s, uint32_t it, in
 #pragma unroll
   for (int l = 0; l < LAG_MAX; ++l) {
     const int sp = s - 1 - l;  // the earlier block
-    if (l >= nlist || sp < d.seg0 || (persistent && d.rcorr)) continue;  // (rcorr: the reducers subtract it)
+    // (rcorr: the reducers subtract it -- all but block s-1's with rcsplit)
+    if (l >= nlist || sp < d.seg0 || (persistent && d.rcorr && !(d.rcsplit && l == 0))) continue;
     const int gp = d.gblk[sp];
     if (l == 0)
       Cl[l] = (gb == (gp + 1) % d.nb) ? d.xgram + (int64_t)gp * B * B : d.xgramT + (int64_t)gb * B * B;
@@ -4061,7 +4062,7 @@ __device__ __forceinline__ void reduce_role(const Dev &d, int r, int nsg, int nr
       double cor[LAG_MAX] = {0.0, 0.0, 0.0};
       for (int l = LAG_MAX - 1; l >= 0; --l) {  // (the older lists are published first)
         const int sp = s - 1 - l;
-        if (l >= lag || sp < d.seg0) continue;
+        if (l >= lag || sp < d.seg0 || (d.rcsplit && l == 0)) continue;  // (rcsplit: the solver corrects for s-1)
         if (t == 0) wait_geq(d.sync + SY_PEND, d.sbase + sp + 1, d.sync, 7);
         __syncthreads();  // (also: the partial sums above are consumed)
         const int slot = sp % NSLOT;

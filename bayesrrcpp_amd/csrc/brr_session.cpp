@@ -501,6 +501,10 @@ int do_sweep_local(brr_session *s) {
       // profiles/r05i_ab.log, r05g*); BRR_RED_PF=1 turns it on where the slices fit a reducer's LDS
       const char *pf = getenv("BRR_RED_PF");
       dp.rcpf = dp.rcorr && s->fused.rcpf && pf && pf[0] == '1';
+      // BRR_RED_SPLIT=1: the newest list's correction in the solver (its own list, from its LDS), the
+      // older ones in the reducers
+      const char *sp = getenv("BRR_RED_SPLIT");
+      dp.rcsplit = dp.rcorr && sp && sp[0] == '1';
     }
     dp.slab_storage = d.Xc != nullptr || d.xcodes != nullptr;  // streamers read blocks in storage order (2-bit, f32 code cache)
     FusedCfg fc = s->fused;
