@@ -3254,27 +3254,6 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
       }
       s_pd[e] = pde;
     }
-    if (XF) {
-      // the pair tables: entries 2q and 2q + 1 add W[c0 | c1 << 2] = (x0(c0) d0) + (x1(c1) d1) per row,
-      // the f32 path's (x0 d0 + x1 d1) (the same rounded products, then the same adds); an entry
-      // without a real partner (2q + 1 >= nr) adds x0(c0) d0 alone, as the f32 path does.  (This
-      // wave's LDS writes above are visible to its own reads below: LDS operations of a wave complete
-      // in order.)
-      for (int q = lane; 2 * q < np; q += 64) {
-        const int e = 2 * q;
-        const double *l0 = lutb + 4 * s_ppos[e], *l1 = lutb + 4 * s_ppos[e + 1];
-        const double d0 = s_pd[e], d1 = s_pd[e + 1];
-        const bool single = e + 1 >= nr;
-        double w0[4], w1[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) { w0[k] = l0[k] * d0; w1[k] = l1[k] * d1; }
-        double *wq = s_w + 16 * q;
-#pragma unroll
-        for (int c1 = 0; c1 < 4; ++c1)
-#pragma unroll
-          for (int c0 = 0; c0 < 4; ++c0) wq[c0 + 4 * c1] = single ? w0[c0] : w0[c0] + w1[c1];
-      }
-    }
     // (table storage) dense: the list is the block's first nr columns in storage order -- the
     // Horseshoe's every block (the solver writes lists in storage order, solve_block)
     bool dn = true;
@@ -3288,6 +3267,17 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
   const int nr_d = __builtin_amdgcn_readfirstlane(s_np[1]);
   const int nr = nr_d & ((1 << 30) - 1);
   const bool dense = XF && (nr_d >> 30) != 0;
+  if (XF && np > 0) {
+    // the pair tables, by every thread: entries 2q and 2q + 1 add W[c0 | c1 << 2] = (x0(c0) d0) + (x1(c1) d1)
+    // per row, the f32 path's (x0 d0 + x1 d1) (the same rounded products, then the same adds); an entry
+    // without a real partner (2q + 1 >= nr) adds x0(c0) d0 alone, as the f32 path does
+    for (int i = t; i < 8 * np; i += NT) {
+      const int e = 2 * (i >> 4), c0 = i & 3, c1 = (i >> 2) & 3;
+      const double w0 = lutb[4 * s_ppos[e] + c0] * s_pd[e];
+      s_w[i] = e + 1 >= nr ? w0 : w0 + lutb[4 * s_ppos[e + 1] + c1] * s_pd[e + 1];
+    }
+    __syncthreads();
+  }
   const uint64_t tq1 = ptime ? wall_clock64() : 0;
   const int G = apply_nparts(np, npass);  // parts of the list
   const int ldp = npass * SROWS;                          // doubles per part in s_part
