@@ -1378,10 +1378,14 @@ __device__ __forceinline__ FastDec decide_fast(double r, const double *a, const 
 // re-decision, wave-uniform arguments): component k on lane k, so the K exponentials and the K quotients
 // of the softmax issue once, side by side, instead of K times on the chain.  Every element is the same
 // operation on the same values as in decide_fast and every sum runs in the same order (maxima and minima
-// are exact in any order): the result is bit-identical to decide_fast's.
-__device__ __forceinline__ FastDec decide_fast_wave(double r, const double *a, const double *den, int64_t stride, int K,
+// are exact in any order): the result is bit-identical to decide_fast's.  KT > 0: K = KT known at compile
+// time (the loops over components lose their per-component branches: the default K = 4 runs this form).
+template <int KT = 0>
+__device__ __forceinline__ FastDec decide_fast_wave(double r, const double *a, const double *den, int64_t stride, int Kr,
                                                     double sigmaE, double p) {
 #pragma clang fp contract(off)
+  constexpr int KM = KT > 0 ? KT : MAXK;
+  const int K = KT > 0 ? KT : Kr;
   FastDec o;
   o.ex = false;
   const double t = r * r;
@@ -1393,7 +1397,7 @@ __device__ __forceinline__ FastDec decide_fast_wave(double r, const double *a, c
   const double Lk = a[kl * stride] + sl * t;
   double mx = -1e308, mn = 1e308, smax = 0.0;
 #pragma unroll
-  for (int k = 0; k < MAXK; ++k) {
+  for (int k = 0; k < KM; ++k) {
     if (k < K) {
       const double v = readlane_f64(Lk, k);
       mx = fmax(mx, v);
@@ -1403,14 +1407,14 @@ __device__ __forceinline__ FastDec decide_fast_wave(double r, const double *a, c
   }
   if (!(mx - mn < 690.0) || !(smax > 0.0)) { o.ex = true; o.k = 0; o.lo = 1.0; o.hi = -1.0; return o; }
   const double ek = exp(Lk - mx);
-  double S = 0.0, ev[MAXK];
+  double S = 0.0, ev[KM];
 #pragma unroll
-  for (int k = 0; k < MAXK; ++k) {
+  for (int k = 0; k < KM; ++k) {
     if (k < K) { ev[k] = readlane_f64(ek, k); S += ev[k]; }
   }
   double acc = 0.0, myacc = 0.0;
 #pragma unroll
-  for (int k = 0; k < MAXK; ++k) {
+  for (int k = 0; k < KM; ++k) {
     if (k < K) {
       acc += ev[k];
       myacc = kl == k ? acc : myacc;
@@ -1420,7 +1424,7 @@ __device__ __forceinline__ FastDec decide_fast_wave(double r, const double *a, c
   int sel = FALLTHROUGH;
   double Asel = 0.0, Aprev = 0.0, Al = 0.0;
 #pragma unroll
-  for (int k = 0; k < MAXK; ++k) {
+  for (int k = 0; k < KM; ++k) {
     if (k < K) {
       const double A = readlane_f64(Ak, k);
       if (sel == FALLTHROUGH && p <= A) { sel = k; Asel = A; Aprev = Al; }
@@ -1482,11 +1486,12 @@ __device__ __noinline__ Decision decide_bayesr_ool(double num, double xsq, doubl
 }
 // decide_pos for the chains (a whole wave, uniform arguments): the fast decision inline and spread over the
 // K lanes, the exact fallback out of line
+template <int KT = 0>
 __device__ __forceinline__ FastDec decide_pos_ool(const int *gAssign, const double *sigmaGG, const double *pi,
                                                   const double *cva, int G, int K, double r, const double *a,
                                                   const double *den, int64_t stride, double sigmaE, double p,
                                                   double x2, int m) {
-  FastDec o = decide_fast_wave(r, a, den, stride, K, sigmaE, p);
+  FastDec o = decide_fast_wave<KT>(r, a, den, stride, K, sigmaE, p);
   if (o.ex) {
     const int g = gAssign ? gAssign[m] : 0;
     Decision dc = decide_bayesr_ool(r, x2, sigmaE, sigmaGG[g], pi + (int64_t)g * K, cva + g, G, K, p, true);
@@ -1499,6 +1504,31 @@ __device__ __forceinline__ FastDec decide_pos_ool(const int *gAssign, const doub
     }
   }
   return o;
+}
+
+// A serial chain's re-decision of position `first` (a whole wave, uniform arguments).  K = 4 (the default
+// mixture) runs the compile-time form of decide_fast_wave; BRR_DECIDE_K4 = 0 keeps the runtime-K form for
+// every K, 2 moves the runtime-K form out of line.
+#ifndef BRR_DECIDE_K4
+#define BRR_DECIDE_K4 1
+#endif
+__device__ __noinline__ FastDec decide_pos_generic_ool(const int *gAssign, const double *sigmaGG, const double *pi,
+                                                       const double *cva, int G, int K, double r, const double *a,
+                                                       const double *den, int64_t stride, double sigmaE, double p,
+                                                       double x2, int m) {
+  return decide_pos_ool(gAssign, sigmaGG, pi, cva, G, K, r, a, den, stride, sigmaE, p, x2, m);
+}
+__device__ __forceinline__ FastDec chain_redecide(const Dev &d, double rf, const double *a, const double *den,
+                                                  int64_t stride, double sigmaE, double p, double x2, int m) {
+#if BRR_DECIDE_K4 == 1
+  return d.K == 4 ? decide_pos_ool<4>(d.gAssign, d.sigmaGG, d.pi, d.cva, d.G, 4, rf, a, den, stride, sigmaE, p, x2, m)
+                  : decide_pos_ool(d.gAssign, d.sigmaGG, d.pi, d.cva, d.G, d.K, rf, a, den, stride, sigmaE, p, x2, m);
+#elif BRR_DECIDE_K4 == 2
+  return d.K == 4 ? decide_pos_ool<4>(d.gAssign, d.sigmaGG, d.pi, d.cva, d.G, 4, rf, a, den, stride, sigmaE, p, x2, m)
+                  : decide_pos_generic_ool(d.gAssign, d.sigmaGG, d.pi, d.cva, d.G, d.K, rf, a, den, stride, sigmaE, p, x2, m);
+#else
+  return decide_pos_ool(d.gAssign, d.sigmaGG, d.pi, d.cva, d.G, d.K, rf, a, den, stride, sigmaE, p, x2, m);
+#endif
 }
 
 // ------------------------------------------------------------------------------------
@@ -1862,6 +1892,21 @@ __device__ __forceinline__ double quot_rn(double num, double den, double inv) {
   return __builtin_fma(__builtin_fma(-q0, den, num), inv, q0);
 }
 
+// The new-beta arms of a chain's re-decision: lane c < K holds quot_rn(num, D_c) + sqrt(sigmaE / D_c) z, the
+// new beta if component c >= 1 is drawn (BayesRv2.cpp:226-230) -- the operations the chain's fast step
+// applies to the selected component's constants, on the same values, formed beside the decision (off its
+// dependency chain); the decision picks one arm by a readlane.  The chains need nothing else of the
+// selected component: a re-decided position is stepped at once or left, never examined again.
+__device__ __forceinline__ double refresh_arm(double num, const double *den, int64_t stride, int K, double sigmaE,
+                                              double z) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  const int kl = lane < K ? lane : 0;
+  const double dk = kl >= 1 ? den[(kl - 1) * stride] : 1.0;
+  const double iv = 1.0 / dk;
+  return quot_rn(num, dk, iv) + sqrt(sigmaE / dk) * z;
+}
+
 // Resident-Gram serial chain, Horseshoe (wave 0).  Every position changes
 // (beta ~ N(num/D, sigmaE/D), HorseshoeR.cpp:226-234): a forward substitution through the block in
 // position order,
@@ -2162,32 +2207,43 @@ __device__ __forceinline__ void chain_bayesr_resident_blk(const Dev &d, int bs, 
         const double rf = readlane_f64(r[k], L);
         const bool exf = (__builtin_amdgcn_readlane((int)exb, L) >> k) & 1;
         if (!exf) {
-          // outside its window: re-decide at the current num, then re-examine
-          FastDec o = decide_pos_ool(d.gAssign, d.sigmaGG, d.pi, d.cva, d.G, d.K, rf, La + first, Lden + first, B, sigmaE,
-                                     Lp[first], Lx2[first], Lm[first]);
-          const bool lk = o.ex || !(o.k == FALLTHROUGH || (o.k == 0 && readlane_f64(bo[k], L) == 0.0));
-          const double dsel = (!o.ex && o.k >= 1 && o.k != FALLTHROUGH) ? Lden[(o.k - 1) * B + first] : 1.0;
-          const double sdz = sqrt(sigmaE / dsel) * Lz[first];
+          // outside its window: re-decide at the current num.  A fast decision that changes the position is
+          // its step at once (the re-examination would find it inside its new window and take the fast arm
+          // with these constants: the same delta); the exact formula's cases are re-examined
+          const double arm = refresh_arm(rf, Lden + first, B, d.K, sigmaE, Lz[first]);
+          const double pf = Lp[first], x2f = Lx2[first];
+          const int mf = Lm[first];
+          FastDec o = chain_redecide(d, rf, La + first, Lden + first, B, sigmaE, pf, x2f, mf);
+          const double bof = readlane_f64(bo[k], L);
+          const bool lk = o.ex || !(o.k == FALLTHROUGH || (o.k == 0 && bof == 0.0));
+          // (its D, 1 / D and noise are not needed again: the position is stepped now or left)
           if (lane == L) {
-            lo[k] = o.lo; hi[k] = o.hi; ks[k] = o.k; dv[k] = dsel; iv[k] = 1.0 / dsel; sz[k] = sdz;
+            lo[k] = o.lo; hi[k] = o.hi; ks[k] = o.k;
             act = (act & ~bk) | ((uint32_t)lk << k);
             win = (win & ~bk) | ((uint32_t)(!o.ex) << k);
             exb = (exb & ~bk) | ((uint32_t)o.ex << k);
           }
           ++nref;
+          if (o.ex || !lk) {
+            if (prof) tslow += wall_clock64() - ts0;
+            continue;
+          }
+          const double bnr = o.k == 0 ? 0.0 : readlane_f64(arm, o.k);
+          bn[k] = lane == L ? bnr : bn[k];
+          delta = bnr - bof;
           if (prof) tslow += wall_clock64() - ts0;
-          continue;
+        } else {
+          const double bof = readlane_f64(bo[k], L);
+          const int m = Lm[first];
+          const int g = d.gAssign ? d.gAssign[m] : 0;
+          Decision dc = decide_bayesr_ool(rf, Lx2[first], sigmaE, d.sigmaGG[g], d.pi + (int64_t)g * d.K, d.cva + g, d.G,
+                                          d.K, Lp[first], false);
+          const double bnf = dc.k == 0 ? 0.0 : (dc.k == FALLTHROUGH ? bof : rf / dc.denom + sqrt(sigmaE / dc.denom) * Lz[first]);
+          if (lane == L) { bn[k] = bnf; ks[k] = dc.k; }
+          delta = bnf - bof;
+          ++nslow;
+          if (prof) tslow += wall_clock64() - ts0;
         }
-        const double bof = readlane_f64(bo[k], L);
-        const int m = Lm[first];
-        const int g = d.gAssign ? d.gAssign[m] : 0;
-        Decision dc = decide_bayesr_ool(rf, Lx2[first], sigmaE, d.sigmaGG[g], d.pi + (int64_t)g * d.K, d.cva + g, d.G,
-                                        d.K, Lp[first], false);
-        const double bnf = dc.k == 0 ? 0.0 : (dc.k == FALLTHROUGH ? bof : rf / dc.denom + sqrt(sigmaE / dc.denom) * Lz[first]);
-        if (lane == L) { bn[k] = bnf; ks[k] = dc.k; }
-        delta = bnf - bof;
-        ++nslow;
-        if (prof) tslow += wall_clock64() - ts0;
       }
       // the sub-block's later positions subtract G delta now (the raw Gram block is in LDS); the later
       // sub-blocks' positions at the flush
@@ -2321,7 +2377,9 @@ __device__ __forceinline__ void chain_bayesr_rows(const Dev &d, int bs, double s
       const double rf = readlane_f64(rv, L);
       const bool exf = (__builtin_amdgcn_readlane(fll, L) & PF_EX) != 0;
       if (!exf) {
-        // outside its window: re-decide `first` at its current num (wave-uniform), then re-examine it
+        // outside its window: re-decide `first` at its current num (wave-uniform), then re-examine it (the
+        // re-decision's runtime-K form: at B = 256 / 512 re-decisions are rare, and the compile-time form's
+        // registers spill in this kernel)
         const uint64_t tr0 = prof ? wall_clock64() : 0;
         FastDec o = decide_pos_ool(d.gAssign, d.sigmaGG, d.pi, d.cva, d.G, d.K, rf, La + first, Lden + first, B, sigmaE,
                                    Lp[first], Lx2[first], Lm[first]);
