@@ -1374,6 +1374,91 @@ __device__ __forceinline__ FastDec decide_fast(double r, const double *a, const 
   return o;
 }
 
+// quad_perm DPP move of a double within each group of four lanes (CTRL = sel0 | sel1 << 2 | sel2 << 4 |
+// sel3 << 6): a VALU operation, no round trip through a scalar register as a readlane takes
+template <int CTRL>
+__device__ __forceinline__ double quad_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readfirstlane_f64(double v) {
+  const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+  const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+
+// decide_fast for ONE position and K = 4, on a whole wave with every lane active: every quad of lanes holds
+// the four components (component k on lane 4 j + k), maxima and minima run as two quad exchanges, and the
+// exponentials, cumulative sums and side widths reach every lane of the quad by quad broadcasts; each lane
+// then sums in component order.  Element operations, their order and the sums' order are decide_fast's
+// (BayesRv2.cpp:206-220; maxima and minima are exact in any order): bit-identical results, and every quad
+// computes the same values, so the outputs are taken from the first lane.
+__device__ __forceinline__ FastDec decide_fast_quad(double r, const double *a, const double *den, int64_t stride,
+                                                    double sigmaE, double p) {
+#pragma clang fp contract(off)
+  FastDec o;
+  o.ex = false;
+  const double t = r * r;
+  const int kl = threadIdx.x & 3;
+  const double dk = den[(max(kl, 1) - 1) * stride];
+  const double sl = kl == 0 ? 0.0 : 0.5 / (dk * sigmaE);
+  const double Lk = a[kl * stride] + sl * t;
+  double mx = fmax(Lk, quad_f64<0xB1>(Lk));
+  mx = fmax(-1e308, fmax(mx, quad_f64<0x4E>(mx)));
+  double mn = fmin(Lk, quad_f64<0xB1>(Lk));
+  mn = fmin(1e308, fmin(mn, quad_f64<0x4E>(mn)));
+  double smax = fmax(sl, quad_f64<0xB1>(sl));
+  smax = fmax(0.0, fmax(smax, quad_f64<0x4E>(smax)));
+  if (__builtin_amdgcn_readfirstlane((int)(!(mx - mn < 690.0) || !(smax > 0.0)))) {
+    o.ex = true; o.k = 0; o.lo = 1.0; o.hi = -1.0;
+    return o;
+  }
+  const double ek = exp(Lk - mx);
+  const double e0 = quad_f64<0x00>(ek), e1 = quad_f64<0x55>(ek), e2 = quad_f64<0xAA>(ek), e3 = quad_f64<0xFF>(ek);
+  double S = 0.0;
+  S += e0; S += e1; S += e2; S += e3;
+  double acc = 0.0, myacc;
+  acc += e0; myacc = acc;
+  acc += e1; myacc = kl == 1 ? acc : myacc;
+  acc += e2; myacc = kl == 2 ? acc : myacc;
+  acc += e3; myacc = kl == 3 ? acc : myacc;
+  const double Ak = myacc / S;  // lane 4 j + k: A[k]
+  const double A[4] = {quad_f64<0x00>(Ak), quad_f64<0x55>(Ak), quad_f64<0xAA>(Ak), quad_f64<0xFF>(Ak)};
+  int sel = FALLTHROUGH;
+  double Asel = 0.0, Aprev = 0.0, Al = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool hit = sel == FALLTHROUGH && p <= A[k];
+    Asel = hit ? A[k] : Asel;
+    Aprev = hit ? Al : Aprev;
+    sel = hit ? k : sel;
+    Al = A[k];
+  }
+  const double E = 2.718281828459045;
+  // the side above p on even lanes, the side below on odd lanes, exchanged by one quad move
+  const bool below = (threadIdx.x & 1) != 0;
+  const double gap = below ? p - Aprev : Asel - p;
+  const double Ag = below ? Aprev : Asel;
+  double sw;
+  if (!(gap > 1e-12)) sw = 0.0;
+  else {
+    const double m = fmin(Ag, 1.0 - Ag);
+    sw = m > 0.0 ? gap / (E * smax * m) : 1e300;
+  }
+  const double swo = quad_f64<0xB1>(sw);
+  const double sw0 = below ? swo : sw, sw1 = below ? sw : swo;
+  const double ism = 1.0 / smax;
+  double w = sel == FALLTHROUGH ? 0.0 : (sel > 0 ? fmin(sw0, sw1) : sw0);
+  w = fmin(w, ism);
+  const double mg = readfirstlane_f64(0.5 * w);
+  o.k = __builtin_amdgcn_readfirstlane(sel);
+  if (!(mg > 0.0)) { o.ex = true; o.lo = 1.0; o.hi = -1.0; return o; }
+  o.lo = t - mg;
+  o.hi = t + mg;
+  return o;
+}
+
 // decide_fast for ONE position, evaluated by a whole wave with every lane active (the serial chains'
 // re-decision, wave-uniform arguments): component k on lane k, so the K exponentials and the K quotients
 // of the softmax issue once, side by side, instead of K times on the chain.  Every element is the same
@@ -1384,6 +1469,7 @@ template <int KT = 0>
 __device__ __forceinline__ FastDec decide_fast_wave(double r, const double *a, const double *den, int64_t stride, int Kr,
                                                     double sigmaE, double p) {
 #pragma clang fp contract(off)
+  if constexpr (KT == 4) return decide_fast_quad(r, a, den, stride, sigmaE, p);
   constexpr int KM = KT > 0 ? KT : MAXK;
   const int K = KT > 0 ? KT : Kr;
   FastDec o;
