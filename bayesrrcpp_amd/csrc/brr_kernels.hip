@@ -1374,6 +1374,15 @@ __device__ __forceinline__ FastDec decide_fast(double r, const double *a, const 
   return o;
 }
 
+// The lane index, formed where it is used: the chains' re-decisions index their components' LDS
+// constants by lane, and an index hoisted out of the chain loop is spilled in the solver kernel and its
+// scratch reload (a full vmcnt wait) lands on the re-decision's path (~40 % of C1's re-decision time)
+__device__ __forceinline__ int lane_here() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 // quad_perm DPP move of a double within each group of four lanes (CTRL = sel0 | sel1 << 2 | sel2 << 4 |
 // sel3 << 6): a VALU operation, no round trip through a scalar register as a readlane takes
 template <int CTRL>
@@ -1400,7 +1409,7 @@ __device__ __forceinline__ FastDec decide_fast_quad(double r, const double *a, c
   FastDec o;
   o.ex = false;
   const double t = r * r;
-  const int kl = threadIdx.x & 3;
+  const int kl = lane_here() & 3;
   const double dk = den[(max(kl, 1) - 1) * stride];
   const double sl = kl == 0 ? 0.0 : 0.5 / (dk * sigmaE);
   const double Lk = a[kl * stride] + sl * t;
@@ -1437,7 +1446,7 @@ __device__ __forceinline__ FastDec decide_fast_quad(double r, const double *a, c
   }
   const double E = 2.718281828459045;
   // the side above p on even lanes, the side below on odd lanes, exchanged by one quad move
-  const bool below = (threadIdx.x & 1) != 0;
+  const bool below = (kl & 1) != 0;
   const double gap = below ? p - Aprev : Asel - p;
   const double Ag = below ? Aprev : Asel;
   double sw;
@@ -1986,7 +1995,7 @@ __device__ __forceinline__ double quot_rn(double num, double den, double inv) {
 __device__ __forceinline__ double refresh_arm(double num, const double *den, int64_t stride, int K, double sigmaE,
                                               double z) {
 #pragma clang fp contract(off)
-  const int lane = threadIdx.x & 63;
+  const int lane = lane_here();
   const int kl = lane < K ? lane : 0;
   const double dk = kl >= 1 ? den[(kl - 1) * stride] : 1.0;
   const double iv = 1.0 / dk;
