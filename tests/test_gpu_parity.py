@@ -121,6 +121,22 @@ def test_v2_block64_and_many_sweeps(brr, oracle_mod, require_gpu):
     _compare(s, orc, O, L, L.MODEL_V2, tag="B=64 20 sweeps")
 
 
+@pytest.mark.parametrize("cva", [[1e-3, 1e-2], [1e-4, 1e-3, 1e-2], [1e-4, 1e-3, 3e-3, 1e-2]])
+def test_redecision_heavy_chain(brr, oracle_mod, require_gpu, cva):
+    """Few rows, strong effects: a chain's nums move far and many positions leave their decision
+    windows, so the serial chain re-decides often -- K = 4 through the compile-time quad form
+    (decide_fast_quad, a re-decided change stepped at once), K = 3 and 5 through the runtime-K form --
+    against the oracle, component choices identical, over several sweeps at B = 128."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    X, Y, _ = _cohort(O, 96, 640, n_causal=60)
+    s, orc = _make(brr, O, L.MODEL_V2, X, Y, 0, B=128, cva=cva)
+    for it in range(8):
+        s.sweep(1)
+        orc.sweep(1)
+        _compare(s, orc, O, L, L.MODEL_V2, tag=f"K={len(cva) + 1} it={it}")
+
+
 @pytest.mark.parametrize("xs", ["f32", "2bit"])
 @pytest.mark.parametrize("B", [256, 512])
 def test_v2_large_blocks(brr, oracle_mod, require_gpu, B, xs):
