@@ -110,6 +110,9 @@ int dalloc(T **p, int64_t n) {
   if (n <= 0) n = 1;
   hipError_t e = hipMalloc((void **)p, sizeof(T) * (size_t)n);
   if (e != hipSuccess) {
+    // clear the runtime's sticky last error: a later launcher that returns hipGetLastError() (e.g.
+    // launch_slab_sentinels) would otherwise report this failed allocation as its own launch failure
+    (void)hipGetLastError();
     set_error("hipMalloc(%lld bytes) failed: %s", (long long)(sizeof(T) * n), hipGetErrorString(e));
     return -2;
   }
@@ -993,9 +996,18 @@ int brr_device_memory(int32_t device, int64_t *free_bytes, int64_t *total_bytes)
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n < 1) { set_error("no HIP device available"); return -1; }
   if (device < 0 || device >= n) { set_error("device %d not present", device); return -1; }
-  HIPCHK(hipSetDevice(device));
+  // a query only: the caller's current device is restored on every path
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) prev = device;
   size_t f = 0, t = 0;
-  HIPCHK(hipMemGetInfo(&f, &t));
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipMemGetInfo(&f, &t);
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("HIP error %s: %s (device memory query)", hipGetErrorName(e), hipGetErrorString(e));
+    return -1;
+  }
   if (free_bytes) *free_bytes = (int64_t)f;
   if (total_bytes) *total_bytes = (int64_t)t;
   return 0;
@@ -1062,6 +1074,9 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     delete s;
     return nullptr;
   }
+  // an earlier call's failure (e.g. another session's failed allocation) must not surface as this
+  // session's error: the launchers report hipGetLastError()
+  (void)hipGetLastError();
   hipDeviceProp_t prop;
   (void)hipGetDeviceProperties(&prop, s->device);
   const int cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
@@ -1123,13 +1138,26 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     size_t mfree = 0, mtotal = 0;
     if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess) {
       const double xb = s->x2bit ? (double)d.ldc * s->nb * B + 16.0 * M : 4.0 * (double)d.ld * M;
-      const double grams = 3.0 * 8.0 * (double)s->nb * B * B;  // gram, xgram, xgramT (lag 2 adds two more later)
+      // Gram sets: gram, xgram, xgramT, and for the fused sweep's lag 2 (3) the cross-Gram blocks of
+      // blocks two (three) apart in both orientations -- the lag chosen below, before the fused
+      // geometry is known (the per-block fallback runs lag 1 and leaves these unallocated: an over-count)
+      const char *lg = getenv("BRR_LAG");
+      const char *pb = getenv("BRR_PER_BLOCK");
+      int lag_pre = 1;
+      if (opt.order_mode == BRR_ORDER_BLOCKED && s->nb >= 4 && !rows && !(pb && pb[0] == '1') && !(lg && atoi(lg) < 2))
+        lag_pre = (lg && atoi(lg) >= 3 && s->nb >= 5) ? 3 : 2;
+      const double grams = (3.0 + 2.0 * (lag_pre - 1)) * 8.0 * (double)s->nb * B * B;
+      // the integer Gram's class codes of the layout (N P / 4 bytes, during init; REFERENCE order keeps
+      // them and a column-major copy for every sweep).  Without that memory init would fall back to
+      // the FP64 Gram kernel, ~6x slower, so it is counted too.
+      const double codes = (double)d.ldc * s->nb * B * (opt.order_mode == BRR_ORDER_REFERENCE ? 2.0 : 1.0);
       const double small = 8.0 * (double)d.ld * 3 + 8.0 * (double)s->nb * B * (3 + 2 * K) + 64.0 * M + 8.0 * N * std::max<int64_t>(F, 1);
-      const double need = xb + grams + small;
+      const double need = xb + grams + codes + small;
       if (need > (double)mfree) {
-        set_error("device %d has %.2f GB free of %.2f GB: this session needs %.2f GB (X %.2f GB, Gram blocks %.2f GB, "
-                  "the rest %.2f GB)",
-                  s->device, mfree / 1e9, mtotal / 1e9, need / 1e9, xb / 1e9, grams / 1e9, small / 1e9);
+        set_error("device %d has %.2f GB free of %.2f GB: this session needs %.2f GB (X %.2f GB, %d Gram sets %.2f GB, "
+                  "class codes %.2f GB, the rest %.2f GB)",
+                  s->device, mfree / 1e9, mtotal / 1e9, need / 1e9, xb / 1e9, 1 + 2 * lag_pre, grams / 1e9, codes / 1e9,
+                  small / 1e9);
         delete s;
         return nullptr;
       }
@@ -2125,12 +2153,13 @@ brr_options options_from_caller(const brr_options *in) {
   brr_options o;
   brr_options_default(&o);
   if (in) {
-    // ABI 4 gave exchanges_per_sweep = 0 its automatic meaning (E = 8); an older caller -- ABI 3 with
-    // the field zeroed, ABI 1 / 2 without it -- keeps the one exchange per sweep its header documented
+    // an older caller's struct: only the part its ABI had is read, the rest keeps the defaults.
+    // exchanges_per_sweep = 0 means automatic (E = 8) for every ABI: ABI 3's header documented that
+    // (with "query brr_session_exchanges_per_sweep() and run E rounds" for the hand-driven protocol),
+    // and ABI 1 / 2 structs, which have no such field, get the default
     if (in->abi_version >= 3) o = *in;
     else if (in->abi_version == 2) std::memcpy(&o, in, offsetof(brr_options, exchanges_per_sweep));
     else std::memcpy(&o, in, offsetof(brr_options, row_shard_rank));
-    if (in->abi_version < 4 && (in->abi_version < 3 || o.exchanges_per_sweep == 0)) o.exchanges_per_sweep = 1;
     o.abi_version = BRR_ABI_VERSION;
   }
   if (o.exchanges_per_sweep < 0) o.exchanges_per_sweep = 0;

@@ -90,10 +90,10 @@ typedef struct brr_options {
    * chain within Monte-Carlo error.  1 = north_star's single exchange per sweep (measurably biased
    * from 2 shards on).  Every shard must use the same E.
    * Ignored without column shards.
-   * PROTOCOL BREAK at ABI 4: 0 means automatic (E = 8) only for abi_version >= 4.  A caller built
-   * against ABI 3 (0 = one exchange per sweep) or earlier (no field) gets E = 1, so a loop of one
-   * sweep_local / exchange / sweep_finish round per sweep stays a whole sweep; brr_session_sweep and
-   * distributed.HostExchange query brr_session_exchanges_per_sweep() and run E rounds. */
+   * 0 is automatic for every abi_version (as ABI 3 documented it; ABI 1 / 2 structs have no such
+   * field and get the default).  A caller that drives sweep_local / exchange / sweep_finish itself
+   * queries brr_session_exchanges_per_sweep() and runs E rounds per sweep, as brr_session_sweep and
+   * distributed.HostExchange do; E = 1 keeps one round per sweep. */
   int32_t exchanges_per_sweep;
 } brr_options;
 

@@ -86,7 +86,7 @@ def test_header_compiles_as_c(tmp_path):
 
 def test_options_struct_layout(brr, tmp_path):
     # the ctypes mirror has the C compiler's layout of brr_options (ABI 2: row-shard fields, ABI 3:
-    # exchanges_per_sweep; ABI 4: 0 there means automatic)
+    # exchanges_per_sweep, 0 = automatic)
     from bayesrrcpp_amd import _lib
     o = _lib.options()
     assert o.abi_version == _lib.ABI_VERSION == 4
@@ -107,11 +107,11 @@ def test_options_struct_layout(brr, tmp_path):
     assert got[1:] == [getattr(_lib.Options, f).offset for f in fields]
 
 
-@pytest.mark.parametrize("abi,given,want", [(4, 0, 0), (4, 3, 3), (3, 0, 1), (3, 5, 5), (2, 7, 1), (1, 7, 1)])
-def test_older_abi_keeps_one_exchange_per_sweep(brr, abi, given, want):
-    # ABI 4 made exchanges_per_sweep = 0 automatic (E = 8); a caller built against ABI 3 (0 = one
-    # exchange per sweep) or earlier (no such field: whatever follows its struct is not read) keeps
-    # E = 1, so its one sweep_local / exchange / sweep_finish round per sweep stays a whole sweep
+@pytest.mark.parametrize("abi,given,want", [(4, 0, 0), (4, 3, 3), (3, 0, 0), (3, 5, 5), (2, 7, 0), (1, 7, 0)])
+def test_older_abi_exchanges_per_sweep(brr, abi, given, want):
+    # exchanges_per_sweep = 0 is automatic (E = 8) for every ABI, as ABI 3's header documented it; a
+    # caller built against ABI 1 / 2 has no such field (whatever follows its struct is not read) and
+    # gets that default
     from bayesrrcpp_amd import _lib
     L = brr.lib()
     o = _lib.options(block_size=256, shard_count=2)

@@ -6,12 +6,14 @@ the C5-rank test (250 GB of X) had failed an assertion and its session stayed al
 traceback, so the next test's 200 GB create could not fit.  Both paths are run in a child process
 (a crash there fails this test instead of ending the GPU suite):
 * the preflight (default): free HBM checked against the big buffers before anything is allocated;
-* BRR_NO_MEM_PREFLIGHT=1: the allocations themselves.  Measured on the MI355X box (ROCm 7.2,
-  gpurun_out/r05a_gpu_tests.log): the oversized create returns NULL, but the process's HIP context
-  is broken afterwards -- the next, small, create fails at its first kernel launch ("cannot initialise
-  the dot slots").  A later session of a broken context is the round-4 failure mode, and the reason
-  the preflight exists.  This variant checks only that the oversized create returns NULL instead of
-  crashing, and records its message.
+* BRR_NO_MEM_PREFLIGHT=1: the allocations themselves.  Round 5 saw the next, small, create fail
+  at its first kernel launch ("cannot initialise the dot slots", gpurun_out/r05a_gpu_tests.log) and
+  read it as a broken HIP context.  It was the runtime's sticky last error: the failed hipMalloc left
+  hipErrorOutOfMemory behind, and the next session's first launcher returns hipGetLastError().  The
+  library now clears it where an allocation fails and at every create, so both variants require the
+  same: NULL with the reason, then a working chain.
+A third case is sized inside what the round-5 preflight missed (the lag-2 cross-Gram sets of blocks
+two apart and the integer Gram's class codes): X and three Gram sets fit, the whole session does not.
 """
 import json
 import os
@@ -42,8 +44,14 @@ M_alive = int(0.4 * total / (4 * 100_096)) // 512 * 512
 a = Session(L.MODEL_V2, N, M_alive, K=4)
 free1, _ = L.device_memory(0)
 out["free_with_alive"] = free1
-# a second session whose X alone is 10 GB more than what is free
-M_big = int((free1 + 10e9) / (4 * 100_096)) // 512 * 512 + 512
+if sys.argv[2] == "gap":
+    # X + gram / xgram / xgramT fit (412,800 B per marker), X + five Gram sets + class codes do not
+    # (~446,000 B per marker): the round-5 preflight let this one through
+    M_big = int(free1 / 430_000) // 512 * 512
+else:
+    # a second session whose X alone is 10 GB more than what is free
+    M_big = int((free1 + 10e9) / (4 * 100_096)) // 512 * 512 + 512
+out["M_big"] = M_big
 try:
     Session(L.MODEL_V2, N, M_big, K=4)
     step("big", "created")
@@ -68,12 +76,13 @@ print("RESULT " + json.dumps(out))
 """
 
 
-@pytest.mark.parametrize("preflight", [True, False])
-def test_create_beyond_free_hbm_fails_cleanly(brr, require_gpu, preflight):
+@pytest.mark.parametrize("preflight,size", [(True, "x"), (False, "x"), (True, "gap")])
+def test_create_beyond_free_hbm_fails_cleanly(brr, require_gpu, preflight, size):
     env = dict(os.environ)
     if not preflight:
         env["BRR_NO_MEM_PREFLIGHT"] = "1"
-    r = subprocess.run([sys.executable, "-c", CHILD, REPO], capture_output=True, text=True, env=env, timeout=300)
+    r = subprocess.run([sys.executable, "-c", CHILD, REPO, size], capture_output=True, text=True, env=env,
+                       timeout=300)
     steps = {}
     for ln in r.stdout.splitlines():
         if ln.startswith("STEP "):
@@ -81,12 +90,15 @@ def test_create_beyond_free_hbm_fails_cleanly(brr, require_gpu, preflight):
     # never a crash (SIGSEGV / abort): a failed create returns NULL with the reason
     assert r.returncode in (0, 1), f"child exited {r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}"
     assert steps.get("big") == "failed", (steps, r.stderr[-2000:])
-    if not preflight:
-        print("no-preflight create:", steps.get("msg"))
-        return
     assert r.returncode == 0, f"child exited {r.returncode}\n{r.stdout[-2000:]}\n{r.stderr[-3000:]}"
     out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1][len("RESULT "):])
-    assert "GB free" in out["msg"] and "needs" in out["msg"], out["msg"]
+    print(f"create (preflight={preflight}, {size}):", out["msg"])
+    if preflight:
+        assert "GB free" in out["msg"] and "needs" in out["msg"], out["msg"]
+        if size == "gap":
+            assert "5 Gram sets" in out["msg"] and "class codes" in out["msg"], out["msg"]
+    else:
+        assert "hipMalloc" in out["msg"], out["msg"]
     # nothing of the failed session stays allocated, and the library keeps running chains
     assert abs(out["free_after"] - out["free_with_alive"]) < 1e9, out
     assert out["sigmaE"] > 0

@@ -597,8 +597,9 @@ def test_recycled_device_memory(brr, oracle_mod, require_gpu):
 @pytest.mark.parametrize("lag", [1, 2, 3])
 @pytest.mark.parametrize("model", [0, 1, 2, 3])  # V2, Groups, restart, Horseshoe
 def test_pipeline_lag_all_models(brr, oracle_mod, require_gpu, monkeypatch, model, lag, xs):
-    """Every pipeline lag (default: 2 for V2 / restart / Horseshoe, 1 for Groups; 3 is opt-in) for the
-    other models, against the oracle: many blocks, several streaming workgroups."""
+    """Every pipeline lag (default: 2 for every model in BLOCKED order with nb >= 4 -- V2 / restart
+    adaptively, lag 1 in sweeps after one that changed many markers; 3 is opt-in) for every model,
+    against the oracle: many blocks, several streaming workgroups."""
     from bayesrrcpp_amd import _lib as L
     O = oracle_mod
     monkeypatch.setenv("BRR_LAG", str(lag))
