@@ -15,7 +15,7 @@ REPO = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libbrr.so")
 SOURCES = ["brr_kernels.hip", "brr_session.cpp", "brr_oneshot.cpp"]
-HEADERS = ["brr_device.hpp", "brr_launch.hpp", "brr_rng.hpp", "brr_chain.hpp", "brr_sample.hpp"]
+HEADERS = ["brr_device.hpp", "brr_launch.hpp", "brr_rng.hpp", "brr_chain.hpp", "brr_sample.hpp", "brr_ovsolve.hpp"]
 ARCH = os.environ.get("BRR_OFFLOAD_ARCH", "gfx950")
 
 

@@ -111,12 +111,17 @@ struct Dev {
                     // lists are published
   int slab_storage; // the partial dots are indexed by in-block storage index, not visit position
                     // (fused sweep on 2-bit code tiles)
+  int ovs;          // (fused sweep, BayesR family, B = 128) the overlapped solver workgroup (brr_ovsolve.hpp):
+                    // block s+1 prepared while block s's chain runs; its corrector forms every cross-Gram
+                    // correction (rcorr = 0)
   uint64_t seed;
   Hyper hyp;
   const float *X;      // f32 storage (x_storage BRR_X_F32), else nullptr
   const uint8_t *Xc;   // 2-bit genotype codes (BRR_X_2BIT), else nullptr: column j at Xc + j ldc,
                        // row i in bits 2(i&3)..2(i&3)+1 of byte i>>2 (PLINK .bed packing)
   const float *xlut;   // [M][4] value of each code of column j (padding rows decode to 0)
+  const uint8_t *Xcm;  // 2-bit storage, fused sweep without an LDS code cache: the codes column-major (ldc
+                       // bytes per column, PLINK packing; k_codes_cm), read by the change-list apply, else nullptr
   int64_t ldc;         // bytes per code column = ld / 4
   // value classes of every column (k_classes): the distinct values of its N rows, ascending, when a
   // column has at most 4 of them (genotype columns, in either storage) -- the integer Gram kernel

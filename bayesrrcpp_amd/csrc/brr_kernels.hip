@@ -314,6 +314,24 @@ __global__ __launch_bounds__(256) void k_codes_tile(const uint8_t *src, uint8_t 
     Xc[code_off(c0 + jj, g, B, ldc)] = src[jj * ldc + g];
 }
 
+// 2-bit storage: a column-major copy of the code tiles (ldc bytes per column, PLINK packing), the source of
+// the streamers' change-list apply where no LDS code cache holds the recent blocks: a wave reads one
+// column's 64 row quads as 64 contiguous bytes instead of one byte of each of 64 16-B tile granules
+// (1 KiB of lines).  Thread = one column and four row quads (one 4-byte word).
+__global__ __launch_bounds__(256) void k_codes_cm(Dev d, uint8_t *xcm) {
+  const int64_t nw = d.ldc / 4;  // words per column (ldc = ld / 4, ld a multiple of 256)
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= nw * ((d.M + 15) / 16 * 16)) return;  // (whole tile groups: the last one may be short)
+  // consecutive threads: the 16 columns of a tile group at the same four quads (their reads share 64 B)
+  const int64_t grp = idx / (16 * nw), rem = idx - grp * 16 * nw;
+  const int64_t wq = rem / 16, col = grp * 16 + rem % 16;
+  if (col >= d.M) return;
+  uint32_t v = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v |= (uint32_t)d.Xc[code_off(col, 4 * wq + k, d.B, d.ldc)] << (8 * k);
+  reinterpret_cast<uint32_t *>(xcm + col * d.ldc)[wq] = v;
+}
+
 // y_i = sum_{causal j} x_ij beta_j  (causal list from the host)
 __global__ __launch_bounds__(256) void k_synth_y(Dev d, const int *cidx, const double *cbeta, int nc,
                                                  double *y) {
@@ -3527,6 +3545,8 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
           auto rload = [&](int e) __attribute__((always_inline)) -> uint32_t {
             if constexpr (LDSC)
               return ((const __attribute__((address_space(3))) uint8_t *)ccode)[s_cb[e] + qo];
+            else if (d.Xcm)  // (the column-major copy: 64 contiguous bytes per wave instead of 64 tile granules)
+              return d.Xcm[(int64_t)s_pidx[e] * d.ldc + (src >> 2)];
             else
               return d.Xc[s_cb[e] + qo];
           };
@@ -4277,6 +4297,21 @@ __device__ BRR_SOLVER_INL void solver_role(const Dev &d, uint32_t it, int nslot,
   }
 }
 
+#include "brr_ovsolve.hpp"
+
+// the persistent solver workgroup: the overlapped form where it applies (Dev::ovs), else solve_block
+// per block
+template <bool HS, int B, int NT = SWEEP_NT>
+__device__ __forceinline__ void solver_any(const Dev &d, uint32_t it, int nslot, char *smem) {
+  if constexpr (!HS && B == OVB && NT == 512) {
+    if (d.ovs) {
+      solver_role_ov<B>(d, it, smem);
+      return;
+    }
+  }
+  solver_role<HS, B, NT>(d, it, nslot, smem);
+}
+
 // XF: 0 f32 storage (with the list prefetch when pfe > 0), 1 2-bit codes, 2 f32 storage with the
 // class-code cache -- the streaming roles of k_sweep_stream<XF> at 512 threads, so that a PMC pass of
 // this form counts the path the two-kernel default times (C2 f32: XF 0 + pfe; C4: XF 2)
@@ -4298,7 +4333,7 @@ __global__ __launch_bounds__(SWEEP_NT, 1) void k_sweep(Dev d, uint32_t it, int n
   __syncthreads();
   if (!s_ok) return;
   if (blockIdx.x == 0) {
-    solver_role<HS, B>(d, it, nslot, smem);
+    solver_any<HS, B>(d, it, nslot, smem);
   } else if ((int)blockIdx.x > nsg) {
     reduce_role(d, (int)blockIdx.x - 1 - nsg, nsg, nred, d.sc->prof_on, reinterpret_cast<double *>(smem));
   } else {
@@ -4347,7 +4382,7 @@ __global__ __launch_bounds__(SOLVE_NT, 1) void k_sweep_solve(Dev d, uint32_t it,
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_ok;
   if (!sweep_census(d, total, &s_ok)) return;
-  solver_role<HS, B, SOLVE_NT>(d, it, nslot, smem);
+  solver_any<HS, B, SOLVE_NT>(d, it, nslot, smem);
 }
 
 // NT = 1024 (2-bit storage, B >= 256): 16 waves per streaming workgroup at <= 128 VGPRs -- four
@@ -4593,6 +4628,12 @@ hipError_t launch_synth_x(const Dev &d, uint64_t ds, hipStream_t st) {
 
 hipError_t launch_synth_y(const Dev &d, const int *cidx, const double *cb, int nc, double *y, hipStream_t st) {
   hipLaunchKernelGGL(k_synth_y, dim3(cdiv64(d.N, 256)), dim3(256), 0, st, d, cidx, cb, nc, y);
+  return hipGetLastError();
+}
+
+hipError_t launch_codes_cm(const Dev &d, uint8_t *xcm, hipStream_t st) {
+  const int64_t n = d.ldc / 4 * ((d.M + 15) / 16 * 16);
+  if (n > 0) hipLaunchKernelGGL(k_codes_cm, dim3((unsigned)cdiv64(n, 256)), dim3(256), 0, st, d, xcm);
   return hipGetLastError();
 }
 
@@ -4914,8 +4955,20 @@ bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc) 
 // Both are plain launches: the in-kernel residency census (every workgroup running before any waits
 // on another, else all leave before touching state) guards the hand-over.  BRR_TEST_CENSUS_EXTRA
 // (tests) raises the census target above the grid to exercise the failed-census exit.
-hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipStream_t st, hipStream_t st_side,
+// the overlapped solver (Dev::ovs, brr_ovsolve.hpp) fits this configuration: BayesR family, B = 128, K <= 4,
+// pipeline lag <= 2, and its LDS layout within the solver workgroup's budget
+bool ov_solver_ok(const Dev &d, const FusedCfg &c) {
+  if (c.nsg == 0 || d.model == MODEL_HORSESHOE || d.B != OVB || d.K > OV_KMAX || d.K < 1 || d.lag > 2) return false;
+  hipFuncAttributes attr;
+  const void *fn = c.split ? solve_kernel(d.model, d.B) : sweep_kernel(d.model, d.B, 0);
+  if (!fn || hipFuncGetAttributes(&attr, fn) != hipSuccess) return false;
+  return OV_LDS + attr.sharedSizeBytes <= SOLVE_LDS_MAX;
+}
+
+hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c_in, hipStream_t st, hipStream_t st_side,
                               hipEvent_t ev_go, hipEvent_t ev_done) {
+  FusedCfg c = c_in;
+  if (d.ovs) c.lds = std::max(c.lds, OV_LDS);
   Dev dd = d;
   if (const char *ex = getenv("BRR_TEST_CENSUS_EXTRA")) dd.abase += atoi(ex);
   int nslot = c.nslot, nsg = c.nsg, rpw = c.rpw, npass = c.npass, nred = c.nred, cc = c.ccache;

@@ -16,6 +16,7 @@ hipError_t launch_synth_x(const Dev &d, uint64_t ds, hipStream_t st);
 hipError_t launch_synth_y(const Dev &d, const int *cidx, const double *cb, int nc, double *y, hipStream_t st);
 hipError_t launch_cast_x(const void *src, bool is_f64, int64_t lds, float *dst, int64_t ldd,
                          int64_t N, int64_t M, hipStream_t st);
+hipError_t launch_codes_cm(const Dev &d, uint8_t *xcm, hipStream_t st);
 hipError_t launch_codes_tile(const uint8_t *src, uint8_t *Xc, int64_t c0, int64_t nc, int64_t ldc, int B,
                              hipStream_t st);
 hipError_t launch_classes(const Dev &d, int *flags, hipStream_t st);
@@ -49,6 +50,7 @@ struct FusedCfg {
   size_t st_lds = 0;  // (split) streaming / reducing workgroups' dynamic LDS
 };
 bool fused_config(const Dev &d, int cus, int max_wg, FusedCfg *cfg, bool f32cc = false);
+bool ov_solver_ok(const Dev &d, const FusedCfg &c);
 // split: the solver kernel on st, the streaming kernel on st_side (ev_go / ev_done order them
 // against st); otherwise one k_sweep grid on st (BRR_FUSED_SINGLE=1: the PMC passes' form)
 hipError_t launch_sweep_fused(const Dev &d, uint32_t it, const FusedCfg &c, hipStream_t st, hipStream_t st_side,

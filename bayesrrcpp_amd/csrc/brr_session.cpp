@@ -508,6 +508,13 @@ int do_sweep_local(brr_session *s) {
       // older ones in the reducers
       const char *sp = getenv("BRR_RED_SPLIT");
       dp.rcsplit = dp.rcorr && sp && sp[0] == '1';
+      // the overlapped solver workgroup (brr_ovsolve.hpp; BayesR family at B = 128, lag <= 2): block
+      // s+1's decisions, Gram block and cross-Gram corrections prepared while block s's chain runs.
+      // BRR_OVS=1 turns it on (being measured); its corrector forms every correction, so the reducers
+      // form none (rcorr = 0) and the dots wait for no list publication
+      const char *ov = getenv("BRR_OVS");
+      dp.ovs = ov && ov[0] == '1' && ov_solver_ok(dp, s->fused);
+      if (dp.ovs) dp.rcorr = dp.rcsplit = dp.rcpf = 0;
     }
     dp.slab_storage = d.Xc != nullptr || d.xcodes != nullptr;  // streamers read blocks in storage order (2-bit, f32 code cache)
     FusedCfg fc = s->fused;
@@ -790,6 +797,27 @@ int coll_init(Coll &c, int32_t seed) {
       }))
     return rc;
   if (int rc = coll_each(c, prepare_classes)) return rc;
+  // 2-bit storage whose streamers keep no LDS code cache (B = 512): a column-major copy of the codes
+  // (N M / 4 bytes) for the change-list apply -- a changed column then costs each streaming workgroup
+  // 64 contiguous bytes per 256 rows instead of a byte of 64 16-B tile granules (C2: ~1.5 GB less
+  // traffic per sweep).  BRR_XCM=0: off.
+  if (int rc = coll_each(c, [](brr_session *s) -> int {
+        Dev &d = s->d;
+        const char *xe = getenv("BRR_XCM");
+        if (!s->x2bit || s->fused.nsg == 0 || s->fused.ccache || (xe && xe[0] == '0')) return 0;
+        if (!d.Xcm) {  // (optional: without the memory the apply reads the tiles, as before)
+          uint8_t *p = nullptr;
+          if (hipMalloc(&p, (size_t)d.ldc * s->M) != hipSuccess) {
+            (void)hipGetLastError();
+            return 0;
+          }
+          s->allocs.push_back(p);
+          d.Xcm = p;
+        }
+        HIPCHK(launch_codes_cm(d, const_cast<uint8_t *>(d.Xcm), s->st));  // (every init: X may be new)
+        return 0;
+      }))
+    return rc;
   if (int rc = coll_grams(c)) return rc;
   if (int rc = coll_each(c, [](brr_session *s) -> int {
         Dev &d = s->d;

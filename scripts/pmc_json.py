@@ -24,6 +24,11 @@ def per_dispatch(d, counter):
                 if r.get("Counter_Name") == counter and ("k_sweep<" in kn or "k_sweep_solve<" in kn or "k_sweep_stream<" in kn):
                     rows.append((int(r.get("Dispatch_Id", 0) or 0), float(r["Counter_Value"]), kn))
     rows.sort()
+    if any("k_sweep_stream<" in k for _, _, k in rows) and not any("k_sweep_solve<" in k for _, _, k in rows):
+        # the two-kernel sweep with only the streaming kernel profiled (--kernel-include-regex
+        # k_sweep_stream): the counters are the device's TCC totals over its dispatch, which the solver
+        # kernel's run lies within (launched first, finished before the streamers' end)
+        return [v for _, v, k in rows], "k_sweep_stream (counters over the two-kernel sweep)"
     if any("k_sweep_stream<" in k for _, _, k in rows):
         # the two-kernel sweep: k_sweep_solve and k_sweep_stream of one sweep are launched back to
         # back (consecutive dispatch ids); a sweep's traffic is the sum of the pair
