@@ -12,31 +12,39 @@
 // write-back -- one after the other, so C3's block period is its ~12 us chain plus ~8 us of hand-over
 // and preparation (profiles/r05k_prof_c3.log).  Here the eight waves of the solver workgroup take
 // roles, and block s+1 is prepared while wave 0 runs block s's chain:
-//   wave 0     block s's chain (chain_bayesr_ov); every change (Gram index, delta) is pushed into an
-//              LDS queue as it is made;
+//   wave 0     block s's chain (chain_bayesr_ov); a change the corrector holds no row for (see wave 1)
+//              goes into an LDS queue as it is made;
 //   wave 1     the corrector: the cross-Gram corrections of block s+1's dots for the changes the
 //              streamed dots have not seen -- block s's, corr_j = sum_{i changed in s} C_ij delta_i
-//              (C = X_s^T X_{s+1}), summed from the queue in chain order while the chain runs (one 16-B
-//              row load per change and lane), and at lag 2 block s-1's -- so the reducers correct nothing
-//              and the dots wait for no list publication;
+//              (C = X_s^T X_{s+1}; the rows of the positions predicted to change are loaded into its
+//              registers while the chain runs), and at lag 2 block s-1's -- so the reducers correct
+//              nothing and the dots wait for no list publication;
 //   wave 2     block s-1's write-back (its change list in Gram-index order, the publish, beta / comp /
 //              sel), then positions 0-63 of block s+1's decisions;
 //   wave 3     positions 64-127 of block s+1's decisions: every lane polls its reduced dot, reads its
 //              constants from HBM and decides at num' = dot + x2 bo (block s's changes not yet in);
+//              once the corrector is done, num = num' - corr, and the positions whose num left its
+//              decision window are decided again at num, side by side (waves 2 and 3);
 //   waves 5-7  block s+1's Gram block into the second LDS buffer as its upper triangle (row a holds
 //              G(a, b) for the Gram indices b >= a rounded down to even: 65 KB instead of 128, every row
 //              16-B aligned, so one 16-B LDS-DMA per row), so that two buffers fit beside the rest;
 //   wave 4     idle (it shares wave 0's SIMD: any work there would take the chain's issue slots).
-// At the block boundary wave 0 starts block s+1's chain at num = num' - corr.  A position whose num
-// left its decision window is re-decided on the chain -- as any position whose num the chain's own
-// updates move -- so the steps and decisions are those of the exact sampler.
+// At the block boundary wave 0 starts block s+1's chain from decisions at the exact num, as solve_block's
+// chain does, so the steps and decisions are those of the exact sampler.
 //
 // Synchronisation inside the workgroup: one barrier per block (after every role's work for it), and
-// LDS words with epochs (block indices, never reset) for the hand-overs inside a block: the queue
-// count (wave 0 -> 1) and "set free" (wave 2 -> 3).  LDS
-// operations of one wave complete in issue order, so an entry written before its count is visible to
-// the wave that has read the count.  Every wait is bounded (the session's protocol error flag).
+// LDS words with epochs (block indices, never reset) for the hand-overs inside a block:
+// the queue count and "chain done" (wave 0 -> 1), "corrections done" (wave 1 -> 2, 3) and "set free"
+// (wave 2 -> 3).  LDS
+// operations of one wave complete in issue order, so data written before a word is visible to the wave
+// that has read the word.  Every wait is bounded (the session's protocol error flag).
 
+#ifndef BRR_OV_RC
+#define BRR_OV_RC 32
+#endif
+#ifndef BRR_OV_SLEEP
+#define BRR_OV_SLEEP 1  // s_sleep units between the LDS polls of the waves that wait beside the chain
+#endif
 constexpr int OVB = 128;                     // block size of the overlapped solver
 constexpr int OV_TRI = OVB * (OVB + 2) / 2;  // stored entries of a Gram block: rows a, columns >= a & ~1
 constexpr int OV_GS = OV_TRI;                // doubles per Gram buffer
@@ -51,7 +59,7 @@ constexpr size_t OV_OFF_QGI = OV_OFF_QDL + 8 * OVB;
 constexpr size_t OV_OFF_MISC = OV_OFF_QGI + 4 * OVB;
 constexpr size_t OV_LDS = OV_OFF_MISC + 32 * 4;
 static_assert(OV_LDS <= SOLVE_LDS_MAX - 64, "overlapped solver LDS");
-enum OvFlag : int { OVF_QN = 0, OVF_QDONE = 1, OVF_FREE = 2 };
+enum OvFlag : int { OVF_QN = 0, OVF_QDONE = 1, OVF_FREE = 2, OVF_CDONE = 3, OVF_CREADY = 4 };
 
 // A block's decision set (two, by block parity): written by the deciders (r0 = num', lo, hi, dsel,
 // sdz, bo, fl, gi, m), read by the chain, which writes bn and (over fl) the selected components for the
@@ -97,31 +105,66 @@ __device__ __forceinline__ void ov_wait(const Dev &d, const int *p, int target, 
       }
       return;
     }
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(BRR_OV_SLEEP);
   }
 }
 
-// Decisions of block b, one position per lane (waves 2 and 3).  The position's Gram index, member and
-// old beta go into the set first, then the reduced dot is
-// polled (the slot holds block b's sentinel until its reducer writes it) and re-armed with the
-// sentinel of its next use, then the decision at num' = dot + x2 bo, constants read from HBM (k_prep's
-// per-sweep constants; solve_block reads the same values from LDS).
-__device__ __forceinline__ void ov_decide(const Dev &d, int b, int pos, OvSet st, double sigmaE,
-                                          unsigned long long *twait) {
+// Decisions of block b, one position per lane (waves 2 and 3), in two passes.  The first, early in block
+// b-1: the position's Gram index, member and old beta into the set, the reduced dot polled (the slot holds
+// block b's sentinel until its reducer writes it) and re-armed with the sentinel of its next use, then the
+// decision at num' = dot + x2 bo (block b-1's changes not yet in; constants from HBM, k_prep's per-sweep
+// values -- solve_block reads the same ones from LDS -- kept in registers).  The second, once the
+// corrector has block b-1's changes: num = num' - corr; a position whose t = num^2 left its window is
+// decided again at num (the windows), all of them side by side, so the chain starts
+// from decisions at the exact num as solve_block's does.
+struct OvPos {
+  bool in;
+  int gi, m;
+  double bo, x2, p, z, r;
+  double av[MAXK], dv[MAXK];  // a_k, D_k (k >= 1 at dv[k - 1])
+};
+
+__device__ __forceinline__ void ov_decision(const Dev &d, const OvPos &P, double r, double sigmaE, OvSet st, int pos) {
 #pragma clang fp contract(off)
+  const FastDec o = decide_pos(d, r, P.av, P.dv, 1, sigmaE, P.p, P.x2, P.m);
+  double dsel = 1.0;
+#pragma unroll
+  for (int k = 1; k < MAXK; ++k)
+    if (!o.ex && o.k == k) dsel = P.dv[k - 1];
+  const bool likely = o.ex || !(o.k == FALLTHROUGH || (o.k == 0 && P.bo == 0.0));
+  st.fl[pos] = (o.k & 0xFF) | (o.ex ? PF_EX : 0) | (likely ? PF_LIKELY : 0);
+  st.r0[pos] = r;
+  st.lo[pos] = o.lo;
+  st.hi[pos] = o.hi;
+  st.dsel[pos] = dsel;
+  st.sdz[pos] = sqrt(sigmaE / dsel) * P.z;  // rnorm(muk, sqrt(sigmaE/denom)) noise
+}
+
+__device__ __forceinline__ OvPos ov_decide(const Dev &d, int b, int pos, OvSet st, double sigmaE,
+                                           unsigned long long *twait) {
+#pragma clang fp contract(off)
+  OvPos P;
   const int bs = d.bsz[b];
-  const bool in = pos < bs;
+  P.in = pos < bs;
   const int64_t S = d.nbB;
   const int64_t q = (int64_t)b * OVB + pos;
   const double *mc = d.mc;
-  const int gi = in ? d.gidx[q] : 0;
-  const int m = in ? d.member[q] : 0;
-  const double bo = in ? mc[MC_BO * S + q] : 0.0;
-  st.gi[pos] = gi;
-  st.m[pos] = m;
-  st.bo[pos] = bo;
+  P.gi = P.in ? d.gidx[q] : 0;
+  P.m = P.in ? d.member[q] : 0;
+  P.bo = P.in ? mc[MC_BO * S + q] : 0.0;
+  P.x2 = P.in ? mc[MC_XSQ * S + q] : 1.0;
+  P.p = P.in ? mc[MC_P * S + q] : 0.5;
+  P.z = P.in ? mc[MC_Z * S + q] : 0.0;
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) {
+    P.av[k] = P.in && k < d.K ? mc[(MC_A + k) * S + q] : 0.0;
+    P.dv[k] = P.in && k + 1 < d.K ? mc[(MC_A + d.K + k) * S + q] : 1.0;
+  }
+  st.gi[pos] = P.gi;
+  st.m[pos] = P.m;
+  st.bo[pos] = P.bo;
   // the dots are by visit position, or by in-block storage index (2-bit codes / the f32 code cache)
-  const int sidx = in && d.slab_storage ? gi : pos;
+  const int sidx = P.in && d.slab_storage ? P.gi : pos;
   const int par = b % NPAR;
   double *slab2 = d.slab2 + par * d.slab2_stride;
   const unsigned long long sent = slab_sentinel(d.sbase + b);
@@ -158,21 +201,27 @@ __device__ __forceinline__ void ov_decide(const Dev &d, int b, int pos, OvSet st
   const int nxt = b + NPAR < d.nb ? d.sbase + b + NPAR : d.sbase + d.nb + b % NPAR;
   const unsigned long long ns = slab_sentinel(nxt);
   for (int g = 0; g < d.NG; ++g) st_sc1_u64(slab2 + (int64_t)g * OVB + sidx, ns);
-  if (in) {
-    const double x2 = mc[MC_XSQ * S + q], p = mc[MC_P * S + q], z = mc[MC_Z * S + q];
-    // num' = x . (eps + x b_old) without block b-1's changes (BayesRv2.cpp:191-193); the chain
-    // subtracts their correction
-    const double r = dsum + x2 * bo;
-    const FastDec o = decide_pos(d, r, mc + MC_A * S + q, mc + (MC_A + d.K) * S + q, S, sigmaE, p, x2, m);
-    const double dsel = (!o.ex && o.k >= 1 && o.k != FALLTHROUGH) ? mc[(MC_A + d.K + o.k - 1) * S + q] : 1.0;
-    const bool likely = o.ex || !(o.k == FALLTHROUGH || (o.k == 0 && bo == 0.0));
-    st.fl[pos] = (o.k & 0xFF) | (o.ex ? PF_EX : 0) | (likely ? PF_LIKELY : 0);
-    st.r0[pos] = r;
-    st.lo[pos] = o.lo;
-    st.hi[pos] = o.hi;
-    st.dsel[pos] = dsel;
-    st.sdz[pos] = sqrt(sigmaE / dsel) * z;  // rnorm(muk, sqrt(sigmaE/denom)) noise
-  }
+  // num' = x . (eps + x b_old) without block b-1's changes (BayesRv2.cpp:191-193)
+  P.r = dsum + P.x2 * P.bo;
+  if (P.in) ov_decision(d, P, P.r, sigmaE, st, pos);
+  return P;
+}
+
+// the second pass (after the corrector's flag): num = num' - corr, re-decided where the window was left
+// (when OV_FOLD_MIN or more of the wave's positions left theirs; else the chain re-decides them)
+constexpr int OV_FOLD_MIN = 3;
+__device__ __forceinline__ void ov_fold(const Dev &d, const OvPos &P, int pos, OvSet st, const double *Lcor,
+                                        double sigmaE) {
+#pragma clang fp contract(off)
+  if (!P.in) return;
+  const double r = P.r - Lcor[P.gi];
+  const double t = r * r;
+  const int fl = st.fl[pos];
+  const bool left = !(fl & PF_EX) && !(t >= st.lo[pos] && t <= st.hi[pos]);
+  // (one or two positions of the wave: the chain's re-decision, ~0.7 us each, costs less than this
+  // pass's ~1.5 us; C1 leaves ~13 per block, C3 ~2)
+  if (left && __popcll(__ballot(left)) >= OV_FOLD_MIN) ov_decision(d, P, r, sigmaE, st, pos);
+  else st.r0[pos] = r;
 }
 
 // Block b's Gram block as the triangle (waves 5-7, wave w of nw): row a (B - (a & ~1) doubles, contiguous
@@ -191,56 +240,74 @@ __device__ __forceinline__ void ov_load_gram(const Dev &d, int b, double *tri, i
 }
 
 // A block's change list kept in the corrector's registers for the next block (lag 2): lane l holds
-// entries l and l + 64 (Gram index, delta), in chain order.
+// entries l and l + 64 (Gram index, delta), in position order.
 struct OvStash {
   int g0 = 0, g1 = 0, n = 0;
   double d0 = 0.0, d1 = 0.0;
 };
 
+constexpr int OV_RC = BRR_OV_RC;  // cross-Gram rows the corrector holds in registers (likely positions; 40 spilled)
+
 // The corrector (wave 1): block s+1's dots minus the changes the streamed dots have not seen, so that the
 // reducers correct nothing (Dev::rcorr = 0) and the dots wait for no list publication:
-//   block s's changes (C = X_s^T X_{s+1}), summed in chain order from the queue as wave 0 pushes them;
-//   at lag 2 also block s-1's (C2 = X_{s-1}^T X_{s+1}), from the registers the last block left them in,
-//   summed at the start of the block while the chain runs.
-// corr = (newest + older), the reducers' association (reduce_role).  Lane l owns block s+1's Gram indices
-// 2l, 2l+1 (one 16-B load of each change's cross-Gram row); batches of up to 8 changes have their loads in
-// flight together.
-__device__ __forceinline__ void ov_correct(const Dev &d, int s, int s0, int lag, OvStash &ost, const int *qn,
-                                           const int *qdone, const double *qdl, const int *qgi, double *Lcor,
+//   at lag 2 block s-1's changes (C2 = X_{s-1}^T X_{s+1}), from the registers the last block left them in,
+//   summed at the start of the block;
+//   block s's changes (C = X_s^T X_{s+1}): the cross-Gram rows of the first OV_RC positions the decisions
+//   predict to change are loaded into registers while the chain runs, and when it ends each is scaled by
+//   its position's delta (zero if it did not change), in position order; a change no register holds (a
+//   position re-decided into a change, or predicted past the first OV_RC) is pushed by the chain into an
+//   LDS queue and summed here as it comes, in chain order.
+// corr = (held + queued) + older.  Lane l owns block s+1's Gram indices 2l, 2l+1 (one 16-B load of each
+// cross-Gram row).  After the chain the queue area is its scratch.
+__device__ __forceinline__ void ov_correct(const Dev &d, int s, int s0, int lag, OvStash &ost, OvSet st,
+                                           const int *qn, const int *qdone, double *qdl, int *qgi, double *Lcor,
                                            unsigned long long *ttail) {
 #pragma clang fp contract(off)
   const int lane = threadIdx.x & 63;
+  const int bs = d.bsz[s];
   const int gp = d.gblk[s], gb = d.gblk[s + 1];
   const double *C = gb == (gp + 1) % d.nb ? d.xgram + (int64_t)gp * OVB * OVB : d.xgramT + (int64_t)gb * OVB * OVB;
-  auto rows8 = [&](const double *Cx, int nb8, auto gi_of, auto dl_of, double &x0, double &x1) __attribute__((always_inline)) {
-    double2 cv[8];
-    double dl[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = min(u, nb8 - 1);
-      dl[u] = dl_of(e);
-      cv[u] = *reinterpret_cast<const double2 *>(Cx + (int64_t)gi_of(e) * OVB + 2 * lane);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (u < nb8) {
-        x0 += cv[u].x * dl[u];
-        x1 += cv[u].y * dl[u];
-      }
+  auto rowld = [&](const double *Cx, int g) __attribute__((always_inline)) -> double2 {
+    return *reinterpret_cast<const double2 *>(Cx + (int64_t)g * OVB + 2 * lane);
   };
+  // the likely positions of block s (the decisions' prediction), in position order: the chain holds the
+  // same rule (chain_bayesr_ov)
+  const int f0 = lane < bs ? st.fl[lane] : 0, f1 = lane + 64 < bs ? st.fl[lane + 64] : 0;
+  const uint64_t lk0 = __ballot(f0 & PF_LIKELY), lk1 = __ballot(f1 & PF_LIKELY);
+  double2 row[OV_RC];
+  {
+    uint64_t m0 = lk0, m1 = lk1;
+#pragma unroll
+    for (int r = 0; r < OV_RC; ++r) {
+      const int p = m0 ? __builtin_ctzll(m0) : (m1 ? 64 + __builtin_ctzll(m1) : -1);
+      if (m0) m0 &= m0 - 1; else if (m1) m1 &= m1 - 1;
+      row[r] = p >= 0 ? rowld(C, st.gi[max(p, 0)]) : make_double2(0.0, 0.0);
+    }
+  }
   // the older list (lag 2): block s-1's changes against block s+1
   double b0 = 0.0, b1 = 0.0;
   if (lag >= 2 && s - 1 >= s0) {
     const int gp2 = d.gblk[s - 1];
     const double *C2 = gb == (gp2 + 2) % d.nb ? d.xgram2 + (int64_t)gp2 * OVB * OVB : d.xgram2T + (int64_t)gb * OVB * OVB;
     for (int e0 = 0; e0 < ost.n; e0 += 8) {
-      rows8(C2, min(8, ost.n - e0),
-            [&](int u) { const int e = e0 + u; return __builtin_amdgcn_readlane(e < 64 ? ost.g0 : ost.g1, e & 63); },
-            [&](int u) { const int e = e0 + u; return readlane_f64(e < 64 ? ost.d0 : ost.d1, e & 63); }, b0, b1);
+      double2 cv[8];
+      double dl[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + min(u, ost.n - e0 - 1);
+        dl[u] = readlane_f64(e < 64 ? ost.d0 : ost.d1, e & 63);
+        cv[u] = rowld(C2, __builtin_amdgcn_readlane(e < 64 ? ost.g0 : ost.g1, e & 63));
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (e0 + u < ost.n) {
+          b0 += cv[u].x * dl[u];
+          b1 += cv[u].y * dl[u];
+        }
     }
   }
-  // the newest list: block s's changes, as the chain makes them
-  double a0 = 0.0, a1 = 0.0;
+  // the queued changes, as the chain pushes them, until it ends
+  double c0 = 0.0, c1 = 0.0;
   int nd = 0;
   uint64_t tdone = 0;
   for (uint32_t n = 0;; ++n) {
@@ -250,7 +317,20 @@ __device__ __forceinline__ void ov_correct(const Dev &d, int s, int s0, int lag,
     const int nq = (v >> 9) == s ? (v & 511) : 0;
     while (nd < nq) {
       const int nb8 = min(8, nq - nd);
-      rows8(C, nb8, [&](int u) { return qgi[nd + u]; }, [&](int u) { return qdl[nd + u]; }, a0, a1);
+      double2 cv[8];
+      double dl[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = nd + min(u, nb8 - 1);
+        dl[u] = qdl[e];
+        cv[u] = rowld(C, qgi[e]);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (u < nb8) {
+          c0 += cv[u].x * dl[u];
+          c1 += cv[u].y * dl[u];
+        }
       nd += nb8;
     }
     if (done) break;
@@ -263,17 +343,50 @@ __device__ __forceinline__ void ov_correct(const Dev &d, int s, int s0, int lag,
       }
       break;
     }
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(BRR_OV_SLEEP);
   }
-  Lcor[2 * lane] = a0 + b0;
-  Lcor[2 * lane + 1] = a1 + b1;
-  // block s's list for block s+2's correction
-  ost.n = nd;
-  ost.g0 = lane < nd ? qgi[lane] : 0;
-  ost.d0 = lane < nd ? qdl[lane] : 0.0;
-  ost.g1 = lane + 64 < nd ? qgi[lane + 64] : 0;
-  ost.d1 = lane + 64 < nd ? qdl[lane + 64] : 0.0;
+  // the held rows, scaled by their positions' deltas (this lane's two positions, read by readlane)
+  const double dl0 = lane < bs ? st.bn[lane] - st.bo[lane] : 0.0;
+  const double dl1 = lane + 64 < bs ? st.bn[lane + 64] - st.bo[lane + 64] : 0.0;
+  double a0 = 0.0, a1 = 0.0;
+  {
+    uint64_t m0 = lk0, m1 = lk1;
+#pragma unroll
+    for (int r = 0; r < OV_RC; ++r) {
+      const int p = m0 ? __builtin_ctzll(m0) : (m1 ? 64 + __builtin_ctzll(m1) : -1);
+      if (m0) m0 &= m0 - 1; else if (m1) m1 &= m1 - 1;
+      if (p >= 0) {
+        const double dl = readlane_f64(p < 64 ? dl0 : dl1, p & 63);  // (0 where the position did not change)
+        a0 += row[r].x * dl;
+        a1 += row[r].y * dl;
+      }
+    }
+  }
+  Lcor[2 * lane] = (a0 + c0) + b0;
+  Lcor[2 * lane + 1] = (a1 + c1) + b1;
   if (ttail && lane == 0 && tdone) *ttail += wall_clock64() - tdone;
+}
+
+// block s's changes, in position order, kept for block s+2's correction (lag 2; after the corrections are
+// handed over, off the block boundary's path; the queue area as scratch)
+__device__ __forceinline__ void ov_stash(const Dev &d, int s, OvSet st, double *qdl, int *qgi, OvStash &ost) {
+  const int lane = threadIdx.x & 63;
+  const int bs = d.bsz[s];
+  const double dl0 = lane < bs ? st.bn[lane] - st.bo[lane] : 0.0;
+  const double dl1 = lane + 64 < bs ? st.bn[lane + 64] - st.bo[lane + 64] : 0.0;
+  const uint64_t ch0 = __ballot(dl0 != 0.0), ch1 = __ballot(dl1 != 0.0);
+  const uint64_t below = (1ull << lane) - 1ull;
+  {
+    const int e0 = __popcll(ch0 & below), e1 = __popcll(ch0) + __popcll(ch1 & below);
+    if (dl0 != 0.0) { qgi[e0] = st.gi[lane]; qdl[e0] = dl0; }
+    if (dl1 != 0.0) { qgi[e1] = st.gi[lane + 64]; qdl[e1] = dl1; }
+  }
+  const int nch = __popcll(ch0) + __popcll(ch1);
+  ost.n = nch;
+  ost.g0 = lane < nch ? qgi[lane] : 0;
+  ost.d0 = lane < nch ? qdl[lane] : 0.0;
+  ost.g1 = lane + 64 < nch ? qgi[lane + 64] : 0;
+  ost.d1 = lane + 64 < nch ? qdl[lane + 64] : 0.0;
 }
 
 // Block w's write-back (wave 2): its change list in Gram-index (storage) order -- the order of
@@ -352,14 +465,14 @@ __device__ __forceinline__ void ov_writeback(const Dev &d, int w, OvSet st) {
 }
 
 // Block s's chain (wave 0): chain_bayesr_resident_blk's steps (sub-blocks of 64 positions, lane l
-// holding positions l + 64 q) on the decision set, from num = num' - corr, with the Gram triangle
-// and each change pushed to the corrector's queue.  The per-component constants (re-decisions, the
-// exact formula) arrive by LDS-DMA issued at the block start and are waited for at their first use.
+// holding positions l + 64 q) on the decision set, with the Gram triangle; the changes the corrector holds
+// no row for into its queue.  The per-component constants (re-decisions, the exact formula) arrive by
+// wave 4's LDS-DMA, waited for at their first use.
 template <int B>
-__device__ __forceinline__ void chain_bayesr_ov(const Dev &d, int s, double sigmaE, OvSet st, const double *Lcor,
-                                                const double *La, const double *Lden, const double *Lp,
-                                                const double *Lx2, const double *Lz, const double *tri, double *qdl,
-                                                int *qgi, int *qn, int *qdone, bool prof) {
+__device__ __forceinline__ void chain_bayesr_ov(const Dev &d, int s, double sigmaE, OvSet st, const double *La,
+                                                const double *Lden, const double *Lp, const double *Lx2,
+                                                const double *Lz, const double *tri, double *qdl, int *qgi, int *qn,
+                                                int *qdone, const int *cready, bool prof) {
 #pragma clang fp contract(off)
   constexpr int NS = B / 64;
   const int lane = threadIdx.x & 63;
@@ -374,7 +487,7 @@ __device__ __forceinline__ void chain_bayesr_ov(const Dev &d, int s, double sigm
     const int fl = in ? st.fl[pos] : 0;
     gg[q] = in ? st.gi[pos] : 0;
     tl[q] = ov_row(gg[q]);
-    r[q] = in ? st.r0[pos] - Lcor[gg[q]] : 0.0;  // block s-1's changes folded in
+    r[q] = in ? st.r0[pos] : 0.0;  // (num: block s-1's changes folded in by the deciders' second pass)
     lo[q] = in ? st.lo[pos] : 1.0;
     hi[q] = in ? st.hi[pos] : -1.0;
     dv[q] = in ? st.dsel[pos] : 1.0;
@@ -388,6 +501,14 @@ __device__ __forceinline__ void chain_bayesr_ov(const Dev &d, int s, double sigm
     act |= (uint32_t)(in && (fl & PF_LIKELY)) << q;
     exb |= (uint32_t)(in && (fl & PF_EX)) << q;
     win |= (uint32_t)(in && tt >= lo[q] && tt <= hi[q]) << q;
+  }
+  // the positions whose cross-Gram row the corrector holds: the first OV_RC predicted ones in position order
+  uint32_t held = 0;
+  {
+    const uint64_t l0 = __ballot(act & 1u), l1 = __ballot((act >> 1) & 1u);
+    const uint64_t below = (1ull << lane) - 1ull;
+    held |= (uint32_t)((act & 1u) && __popcll(l0 & below) < OV_RC);
+    held |= (uint32_t)(((act >> 1) & 1u) && __popcll(l0) + __popcll(l1 & below) < OV_RC) << 1;
   }
   int nslow = 0, nsteps = 0, nref = 0, nq = 0;
   bool cw = false;  // the constants' LDS-DMA waited for
@@ -416,8 +537,8 @@ __device__ __forceinline__ void chain_bayesr_ov(const Dev &d, int s, double sigm
         bn[k] = lane == L ? bnl : bn[k];
       } else {
         const uint64_t ts0 = prof ? wall_clock64() : 0;
-        if (!cw) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!cw) {  // (wave 4's LDS-DMA of this block's constants, issued when the last chain ended)
+          ov_wait(d, cready, s, 16);
           cw = true;
         }
         const double rf = readlane_f64(r[k], L);
@@ -461,14 +582,15 @@ __device__ __forceinline__ void chain_bayesr_ov(const Dev &d, int s, double sigm
       // the sub-block's later positions subtract G delta now (G(gif, g) from the triangle: row gif when g >
       // gif, else row g); the later sub-blocks' positions at the flush
       {
-        const int tg = ov_row(gif);
+        const int tg = __builtin_amdgcn_readlane(tl[k], L);  // (= ov_row(gif))
         const double g = tri[gg[k] > gif ? tg + gg[k] : tl[k] + gif];
         const bool later = lane > L && (valid & bk);
         r[k] = later ? r[k] - g * delta : r[k];
         const double tt = r[k] * r[k];
         win = (win & ~bk) | ((uint32_t)(tt >= lo[k] && tt <= hi[k]) << k);
       }
-      if (delta != 0.0) {  // (a zero delta changes nothing: no list entry, no correction)
+      if (delta != 0.0 && !((__builtin_amdgcn_readlane((int)held, L) >> k) & 1)) {
+        // a change whose row the corrector does not hold: into its queue
         if (lane == 0) {
           ((ov_ldbl *)qdl)[nq] = delta;
           ((ov_lint *)qgi)[nq] = gif;
@@ -476,11 +598,11 @@ __device__ __forceinline__ void chain_bayesr_ov(const Dev &d, int s, double sigm
         ++nq;
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         if (lane == 0) ov_st(qn, (s << 9) | nq);
-        if (k + 1 < NS) {
-          ppos = lane == np ? gif : ppos;
-          pdl = lane == np ? delta : pdl;
-          ++np;
-        }
+      }
+      if (k + 1 < NS && delta != 0.0) {  // (a zero delta subtracts exactly nothing)
+        ppos = lane == np ? gif : ppos;
+        pdl = lane == np ? delta : pdl;
+        ++np;
       }
       i = first + 1;
       ++nsteps;
@@ -506,7 +628,6 @@ __device__ __forceinline__ void chain_bayesr_ov(const Dev &d, int s, double sigm
     const int pos = lane + 64 * q;
     if (pos < bs) { st.bn[pos] = bn[q]; st.fl[pos] = ks[q]; }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the constants' LDS-DMA, if no step waited for it)
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   if (lane == 0) ov_st(qdone, s + 1);
   if (lane == 0 && nslow) atomicAdd(&d.sc->n_slow, (unsigned long long)nslow);
@@ -515,6 +636,45 @@ __device__ __forceinline__ void chain_bayesr_ov(const Dev &d, int s, double sigm
     atomicAdd(&d.sc->prof[7], (unsigned long long)nref);
     atomicAdd(&d.sc->prof[8], (unsigned long long)tslow);
     atomicAdd(&d.sc->prof[9], (unsigned long long)(wall_clock64() - tl0));
+  }
+}
+
+// The chain as a called function (BRR_OV_CHAIN_CALL=1): its own register allocation, its LDS operands as
+// address-space-3 pointers (as chain_hs_call)
+#ifndef BRR_OV_CHAIN_CALL
+#define BRR_OV_CHAIN_CALL 0
+#endif
+template <int B>
+__device__ __attribute__((noinline)) void chain_bayesr_ov_call(
+    const Dev &d, int s, double sigmaE, BRR_LDS double *r0, BRR_LDS double *lo, BRR_LDS double *hi, BRR_LDS double *dsel,
+    BRR_LDS double *sdz, BRR_LDS double *bo, BRR_LDS double *bn, BRR_LDS int *fl, BRR_LDS int *gi, BRR_LDS int *m,
+    BRR_LDS const double *La, BRR_LDS const double *Lden, BRR_LDS const double *Lp, BRR_LDS const double *Lx2,
+    BRR_LDS const double *Lz, BRR_LDS const double *tri, BRR_LDS double *qdl, BRR_LDS int *qgi, BRR_LDS int *qn,
+    BRR_LDS int *qdone, BRR_LDS const int *cready, bool prof) {
+  const OvSet st{from_lds(r0), from_lds(lo), from_lds(hi), from_lds(dsel), from_lds(sdz), from_lds(bo), from_lds(bn),
+                 from_lds(fl), from_lds(gi), from_lds(m)};
+  chain_bayesr_ov<B>(d, s, sigmaE, st, from_lds(La), from_lds(Lden), from_lds(Lp), from_lds(Lx2), from_lds(Lz),
+                     from_lds(tri), from_lds(qdl), from_lds(qgi), from_lds(qn), from_lds(qdone), from_lds(cready), prof);
+}
+
+// Block b's per-component constants (the chain's re-decisions and exact formula): one 1-KiB LDS-DMA per
+// field (a_k, D_k, p, x2, z), issued by wave 4
+__device__ __forceinline__ void ov_consts_dma(const Dev &d, int b, double *Lc) {
+  const int lane = threadIdx.x & 63;
+  const int K = d.K, KD = K > 1 ? K - 1 : 0, nf = K + KD + 3;
+  const int64_t S = d.nbB, q0 = (int64_t)b * OVB;
+  for (int f = 0; f < nf; ++f) {
+    const int mf = f < K + KD ? MC_A + f : f == K + KD ? MC_P : f == K + KD + 1 ? MC_XSQ : MC_Z;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(d.mc + mf * S + q0 + 2 * lane),
+                                     (__attribute__((address_space(3))) void *)(Lc + (int64_t)f * OVB), 16, 0, 0);
+  }
+}
+__device__ __forceinline__ void ov_consts(const Dev &d, int s, bool nxt, double *Lc, int *misc) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's DMA of block s's constants)
+  if ((threadIdx.x & 63) == 0) ov_st(misc + OVF_CREADY, s);
+  if (nxt) {
+    ov_wait(d, misc + OVF_QDONE, s + 1, 17);  // chain s no longer reads them
+    ov_consts_dma(d, s + 1, Lc);
   }
 }
 
@@ -539,35 +699,46 @@ __device__ __forceinline__ void solver_role_ov(const Dev &d, uint32_t it, char *
   const int s0 = d.seg0, s1 = d.seg1;
   unsigned long long *pf = prof ? d.sc->prof : nullptr;
   if (t < 32) misc[t] = -(1 << 24);  // epochs below every block index
-  if (t < B) Lcor[t] = 0.0;           // the launch's first block: no newer changes than its dots
   __syncthreads();
-  // prologue: block s0's decision set and Gram triangle
+  // prologue: block s0's decision set (no newer changes than its dots: num' is num), Gram triangle and
+  // constants
+  if (wv == 4) {
+    ov_consts_dma(d, s0, Lc);
+    lds_barrier();
+  } else {
   if (wv == 2 || wv == 3) {
-    ov_decide(d, s0, (wv - 2) * 64 + lane, ov_set(smem, s0), sigmaE, nullptr);
+    (void)ov_decide(d, s0, (wv - 2) * 64 + lane, ov_set(smem, s0), sigmaE, nullptr);
   } else if (wv >= 5) {
     ov_load_gram(d, s0, ov_tri(smem, s0), wv - 5, 3);
   }
   __syncthreads();
+  }
   uint64_t tprev = 0;
   const int lag = sweep_lag(d);
   OvStash ost;  // (wave 1) the last block's change list
   for (int s = s0; s < s1; ++s) {
     const bool nxt = s + 1 < s1;
     if (wv == 0) {
-      // the block's per-component constants (re-decisions, exact formula): one 1-KiB LDS-DMA per field,
-      // waited for at the chain's first use
-      const int64_t S = d.nbB, q0 = (int64_t)s * B;
-      const int nf = K + KD + 3;
-      for (int f = 0; f < nf; ++f) {
-        const int mf = f < K + KD ? MC_A + f : f == K + KD ? MC_P : f == K + KD + 1 ? MC_XSQ : MC_Z;
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(d.mc + mf * S + q0 + 2 * lane),
-                                         (__attribute__((address_space(3))) void *)(Lc + (int64_t)f * B), 16, 0, 0);
-      }
       const uint64_t tc0 = prof ? wall_clock64() : 0;
-      chain_bayesr_ov<B>(d, s, sigmaE, ov_set(smem, s), Lcor, La, Lden, Lp, Lx2, Lz, ov_tri(smem, s), qdl, qgi,
-                         misc + OVF_QN, misc + OVF_QDONE, prof);
+      const uint64_t tcs0 = prof ? __builtin_amdgcn_s_memtime() : 0;
+#if BRR_OV_CHAIN_CALL
+      {
+        const OvSet st = ov_set(smem, s);
+        chain_bayesr_ov_call<B>(d, s, sigmaE, to_lds(st.r0), to_lds(st.lo), to_lds(st.hi), to_lds(st.dsel), to_lds(st.sdz),
+                                to_lds(st.bo), to_lds(st.bn), to_lds(st.fl), to_lds(st.gi), to_lds(st.m), to_lds(La),
+                                to_lds(Lden), to_lds(Lp), to_lds(Lx2), to_lds(Lz), to_lds((const double *)ov_tri(smem, s)),
+                                to_lds(qdl), to_lds(qgi), to_lds(misc + OVF_QN), to_lds(misc + OVF_QDONE),
+                                to_lds((const int *)(misc + OVF_CREADY)), prof);
+      }
+#else
+      chain_bayesr_ov<B>(d, s, sigmaE, ov_set(smem, s), La, Lden, Lp, Lx2, Lz, ov_tri(smem, s), qdl, qgi, misc + OVF_QN,
+                         misc + OVF_QDONE, misc + OVF_CREADY, prof);
+#endif
       if (prof && lane == 0) {
         const uint64_t tc1 = wall_clock64();
+        const uint64_t tcs = __builtin_amdgcn_s_memtime() - tcs0;  // shader clocks of the chain
+        atomicAdd(&pf[11], (unsigned long long)tcs);
+        atomicAdd(&pf[12], (unsigned long long)tcs);
         atomicAdd(&pf[2], (unsigned long long)(tc1 - tc0));
         if (s > s0) atomicAdd(&pf[0], (unsigned long long)(tc0 - tprev));
         atomicAdd(&pf[5], 1ull);
@@ -578,24 +749,36 @@ __device__ __forceinline__ void solver_role_ov(const Dev &d, uint32_t it, char *
         tprev = tc1;
       }
     } else if (wv == 1) {
-      if (nxt) ov_correct(d, s, s0, lag, ost, misc + OVF_QN, misc + OVF_QDONE, qdl, qgi, Lcor, pf ? &pf[10] : nullptr);
-    } else if (wv == 2) {
-      if (s > s0) {
-        const uint64_t tw0 = prof ? wall_clock64() : 0;
-        ov_writeback(d, s - 1, ov_set(smem, s - 1));
-        if (prof && lane == 0) {
-          const uint64_t tw1 = wall_clock64();
-          atomicAdd(&pf[3], (unsigned long long)(tw1 - tw0));
-          d.trace[(int64_t)(s - 1) * 16 + TR_PUB] = tw1;
-        }
-      }
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      if (lane == 0) ov_st(misc + OVF_FREE, s);  // block s-1's set is free for block s+1
-      if (nxt) ov_decide(d, s + 1, lane, ov_set(smem, s + 1), sigmaE, pf ? &pf[13] : nullptr);
-    } else if (wv == 3) {
       if (nxt) {
+        ov_correct(d, s, s0, lag, ost, ov_set(smem, s), misc + OVF_QN, misc + OVF_QDONE, qdl, qgi, Lcor,
+                   pf ? &pf[10] : nullptr);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (lane == 0) ov_st(misc + OVF_CDONE, s);
+        if (lag >= 2) ov_stash(d, s, ov_set(smem, s), qdl, qgi, ost);
+      }
+    } else if (wv == 2 || wv == 3) {
+      if (wv == 2) {
+        if (s > s0) {
+          const uint64_t tw0 = prof ? wall_clock64() : 0;
+          ov_writeback(d, s - 1, ov_set(smem, s - 1));
+          if (prof && lane == 0) {
+            const uint64_t tw1 = wall_clock64();
+            atomicAdd(&pf[3], (unsigned long long)(tw1 - tw0));
+            d.trace[(int64_t)(s - 1) * 16 + TR_PUB] = tw1;
+          }
+        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (lane == 0) ov_st(misc + OVF_FREE, s);  // block s-1's set is free for block s+1
+      } else if (nxt) {
         ov_wait(d, misc + OVF_FREE, s, 12);
-        ov_decide(d, s + 1, 64 + lane, ov_set(smem, s + 1), sigmaE, nullptr);
+      }
+      if (nxt) {
+        const int pos = (wv - 2) * 64 + lane;
+        const OvPos P = ov_decide(d, s + 1, pos, ov_set(smem, s + 1), sigmaE, pf && wv == 2 ? &pf[13] : nullptr);
+        ov_wait(d, misc + OVF_CDONE, s, 13);  // block s's changes are in the corrector's sums
+        const uint64_t tf0 = prof ? wall_clock64() : 0;
+        ov_fold(d, P, pos, ov_set(smem, s + 1), Lcor, sigmaE);
+        if (prof && wv == 2 && lane == 0) atomicAdd(&pf[14], (unsigned long long)(wall_clock64() - tf0));
       }
     } else if (wv >= 5) {
       if (nxt) {
@@ -603,6 +786,12 @@ __device__ __forceinline__ void solver_role_ov(const Dev &d, uint32_t it, char *
         ov_load_gram(d, s + 1, ov_tri(smem, s + 1), wv - 5, 3);
         if (prof && wv == 5 && lane == 0) atomicAdd(&pf[15], (unsigned long long)(wall_clock64() - tg0));
       }
+    } else {
+      // wave 4 (wave 0's SIMD: only a few instructions): block s's constants have landed -- the flag the
+      // chain's first re-decision waits for -- then, once the chain ends, block s+1's go into the area
+      ov_consts(d, s, nxt, Lc, misc);
+      lds_barrier();  // (no vmcnt wait: the DMA stays in flight across the barrier)
+      continue;
     }
     __syncthreads();
   }

@@ -159,6 +159,7 @@ struct brr_session {
   uint8_t *gram_codes = nullptr;  // k_gram_int's input: class codes of the current Gram layout
   uint8_t *xcls = nullptr;        // REFERENCE order: column-major class codes (Dev::xcls)
   int gram_np_init = 0;           // the Gram kernel of the latest init (Dev::gram_np then)
+  int ovs_last = 0;               // the latest fused launch ran the overlapped solver (brr_ovsolve.hpp)
   double mu0 = 0, sigmaE0 = 0;
   double *ex_eps = nullptr, *ex_stats = nullptr;  // exchange buffers (caller- or session-owned)
   bool ex_owned = false;
@@ -509,12 +510,16 @@ int do_sweep_local(brr_session *s) {
       const char *sp = getenv("BRR_RED_SPLIT");
       dp.rcsplit = dp.rcorr && sp && sp[0] == '1';
       // the overlapped solver workgroup (brr_ovsolve.hpp; BayesR family at B = 128, lag <= 2): block
-      // s+1's decisions, Gram block and cross-Gram corrections prepared while block s's chain runs.
-      // BRR_OVS=1 turns it on (being measured); its corrector forms every correction, so the reducers
-      // form none (rcorr = 0) and the dots wait for no list publication
+      // s+1's decisions, Gram block and cross-Gram corrections prepared while block s's chain runs; its
+      // corrector forms every correction, so the reducers form none (rcorr = 0) and the dots wait for no
+      // list publication.  On by default for Groups, where the hand-over it hides outweighs its slower
+      // chain step: C3 12.63 -> 14.31 sweeps/s; off for V2 / restart, whose chain dominates: C1 229 -> 210,
+      // REFERENCE order 8.5 -> 6.7 (profiles/r06k_ab.log, r06h_ab.log).  BRR_OVS=0|1
+      // overrides
       const char *ov = getenv("BRR_OVS");
-      dp.ovs = ov && ov[0] == '1' && ov_solver_ok(dp, s->fused);
+      dp.ovs = (ov ? ov[0] == '1' : s->model == MODEL_GROUPS) && ov_solver_ok(dp, s->fused);
       if (dp.ovs) dp.rcorr = dp.rcsplit = dp.rcpf = 0;
+      s->ovs_last = dp.ovs;
     }
     dp.slab_storage = d.Xc != nullptr || d.xcodes != nullptr;  // streamers read blocks in storage order (2-bit, f32 code cache)
     FusedCfg fc = s->fused;
@@ -1934,6 +1939,7 @@ int brr_session_get_scalar(brr_session *s, int32_t which, double *out) {
     case 107: *out = (double)s->gram_np_init; return 0;  // Gram kernel: class planes of k_gram_int (0 = FP64 k_gram)
     case 130: *out = (double)s->census_failures; return 0;  // residency census failures so far
     case 131: *out = (double)s->fused.nred; return 0;       // fused sweep: reducer workgroups (column slices)
+    case 132: *out = (double)s->ovs_last; return 0;         // the latest fused launch ran the overlapped solver
     case 109: *out = (double)(s->fused.nsg > 0 ? s->fused.stnt : 0); return 0;  // threads per streaming workgroup
     case 108: *out = (double)(s->fused.nsg > 0 && sc.lag_next >= 2 ? s->d.lag : 1); return 0;  // the next sweep's pipeline lag
     case 110: case 111: case 112: case 113: case 114: case 115: case 116: case 117: case 118: case 119:

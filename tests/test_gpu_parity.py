@@ -965,3 +965,40 @@ def test_2bit_reference_order_matches_oracle(brr, oracle_mod, require_gpu, model
         orc.sweep(1)
         assert np.array_equal(s.vector(L.ORDER), orc.vector(O.V_ORDER)), f"visit order it={it}"
         _compare(s, orc, O, L, model, tag=f"2bit reference model={model} it={it}")
+
+
+@pytest.mark.parametrize("xs", ["f32", "2bit"])
+@pytest.mark.parametrize("lag", [1, 2])
+@pytest.mark.parametrize("ovs", [0, 1])
+@pytest.mark.parametrize("model", [0, 1, 2])  # V2, Groups, restart
+def test_overlapped_solver_both_ways(brr, oracle_mod, require_gpu, monkeypatch, model, ovs, lag, xs):
+    """The overlapped solver workgroup (brr_ovsolve.hpp: block s+1's decisions, Gram triangle and every
+    cross-Gram correction prepared while block s's chain runs; the default for Groups) and the round-5
+    solver (the default for V2 / restart), each forced on every BayesR model, both pipeline lags and
+    storages, against the oracle (BayesRv2.cpp:186-245, BayesRv2Groups.cpp:232-298)."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    monkeypatch.setenv("BRR_OVS", str(ovs))
+    monkeypatch.setenv("BRR_LAG", str(lag))
+    monkeypatch.setenv("BRR_STREAM_WG", "5")
+    N, P = 1500, 1100
+    X, Y, _ = _cohort(O, N, P, n_causal=30)
+    kw = {}
+    if model == L.MODEL_GROUPS:
+        G = 3
+        kw = dict(G=G, gAssign=(np.arange(P) * G // P).astype(np.int32),
+                  fixed=np.linspace(-1, 1, N).reshape(N, 1))
+    elif model == L.MODEL_RESTART:
+        rng = np.random.default_rng(3)
+        comp0 = rng.integers(0, 4, P).astype(np.float64)
+        beta0 = np.where(comp0 > 0, rng.normal(0, 0.02, P), 0.0)
+        kw = dict(restart=dict(mu0=0.01, beta0=beta0, sigmaE0=0.7, sigmaGG0=np.array([0.3]),
+                               eps0=Y - X @ beta0 - 0.01, comp0=comp0))
+    s, orc = _make(brr, O, model, X, Y, 0, B=128, xs=xs, **kw)
+    assert s.scalar(104) > 1  # fused sweep
+    for it in range(4):
+        s.sweep(1)
+        orc.sweep(1)
+        assert s.scalar(132) == ovs
+        _compare(s, orc, O, L, model, tag=f"model={model} ovs={ovs} lag={lag} {xs} it={it}")
+
