@@ -568,9 +568,9 @@ def main():
                 "sweep_hbm_gbs": round(x_bytes / (ms * 1e-3) / 1e9, 1),
                 # what limits this configuration in measurement; frac is
                 # always against the HBM roofline of the algorithmic bytes
-                "limiter": ("solver workgroup's per-block time at lag 1 (dots poll, decisions, write-back drain) and the hand-over latency; the decode-dot is not the bound" if x2 and model not in (L.MODEL_GROUPS, L.MODEL_HORSESHOE)
-                            else "solver workgroup's serial chain" if model == L.MODEL_GROUPS
-                            else "solver's phase A: Gram + cross-Gram blocks (256 KB per block) at one CU's share of HBM, beside a stream that re-reads every column (2x bytes)" if model == L.MODEL_HORSESHOE
+                "limiter": ("solver workgroup per 512-marker block (decisions incl. the dots poll, Gram-row staging, row chain, write-back); the decode-dot is not the bound" if x2 and model not in (L.MODEL_GROUPS, L.MODEL_HORSESHOE)
+                            else "solver workgroup's serial chain (overlapped solver: the next block's decisions, Gram block and corrections prepared beside it)" if model == L.MODEL_GROUPS
+                            else "streaming workgroups: the dense apply of every column from the LDS class-code cache plus the stream; the solver close behind" if model == L.MODEL_HORSESHOE
                             else "HBM stream")}
     if args.trace_sweeps:
         # per-sweep wall time and changed markers of a fresh chain's first sweeps (diagnostic)

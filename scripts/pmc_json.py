@@ -44,6 +44,12 @@ def main():
     wk, _ = per_dispatch(wdir, "WRITE_SIZE")
     if not fk or not wk:
         sys.exit("no k_sweep dispatches in the PMC output")
+    # PMC_GROUP = launches per sweep (column-shard exchange segments: E launches of the marker loop per
+    # sweep); the steady state is then the mean of the last two sweeps' sums
+    grp = int(os.environ.get("PMC_GROUP", "1"))
+    if grp > 1:
+        fk = [sum(fk[i:i + grp]) for i in range(len(fk) % grp, len(fk), grp)]
+        wk = [sum(wk[i:i + grp]) for i in range(len(wk) % grp, len(wk), grp)]
     ss_f = sum(fk[-2:]) / len(fk[-2:])
     ss_w = sum(wk[-2:]) / len(wk[-2:])
     d = {
