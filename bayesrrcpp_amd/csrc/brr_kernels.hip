@@ -917,6 +917,439 @@ __global__ __launch_bounds__(256, NP <= 2 ? 2 : 1) void k_gram_int(Dev d, const 
   }
 }
 
+// The class-pair sum of one Gram entry from its explicit counts n[a][b] (a, b < NP), exactly as
+// k_gram_int forms it: the last class's counts from the per-column class totals, the (NP + 1)^2
+// integer multiples of u_a w_b summed in 128 bits, rounded once.
+template <int NP>
+__device__ __forceinline__ double gram_entry(const int64_t (&ne)[NP][NP], const int *h0, const int *h1, const int *M0,
+                                             const int *M1, const int *E0, const int *E1, int emin0, int emin1, int64_t N) {
+  int64_t n[NP + 1][NP + 1];
+  int64_t hi = 0;
+#pragma unroll
+  for (int a = 0; a < NP; ++a) {
+    int64_t sa = 0;
+#pragma unroll
+    for (int b = 0; b < NP; ++b) {
+      n[a][b] = ne[a][b];
+      sa += n[a][b];
+    }
+    n[a][NP] = h0[a] - sa;
+    hi += h0[a];
+  }
+  int64_t sl = 0;
+#pragma unroll
+  for (int b = 0; b < NP; ++b) {
+    int64_t sb = 0;
+#pragma unroll
+    for (int a = 0; a < NP; ++a) sb += n[a][b];
+    n[NP][b] = h1[b] - sb;
+    sl += n[NP][b];
+  }
+  n[NP][NP] = (N - hi) - sl;
+  __int128 s = 0;
+#pragma unroll
+  for (int a = 0; a <= NP; ++a)
+#pragma unroll
+    for (int b = 0; b <= NP; ++b) {
+      const int64_t m = (int64_t)M0[a] * M1[b];
+      if (n[a][b] != 0 && m != 0) s += (__int128)n[a][b] * m * ((__int128)1 << (E0[a] + E1[b]));
+    }
+  return ldexp((double)s, emin0 + emin1);
+}
+
+// k_gram_int with whole 128-column tiles (NP <= 2, the genotype case; B a multiple of 128): one
+// workgroup of 8 waves per GB_T x GB_T output tile, wave w the output rows 32 (w >> 1) .. + 31 and
+// columns 64 (w & 1) .. + 63 with EVERY plane pair of them in its accumulators (NP^2 x 2 x 4 MFMA
+// tiles), so the epilogue forms G from registers (no count matrix in LDS), and a tile whose two sides
+// are the same columns (a diagonal block's diagonal tiles: every block of a B = 128 Gram set) expands
+// its codes once.  The indicator planes are double-buffered by chunks of GB_KC rows: chunk c + 1 is
+// expanded while chunk c's products run, one barrier per chunk.  Against k_gram_int's 64-column tiles
+// the class-plane expansion -- which bounded it, not the matrix cores -- falls to a third (diagonal
+// blocks) or a half (cross blocks) per MFMA and overlaps the products.  The counts and the exact sums
+// are the same: the blocks are bit-identical (the correctly rounded dot products, tests/test_gpu_gram.py).
+constexpr int GB_T = 128;
+constexpr int GB_KC = 128;
+#ifndef BRR_GB_D
+#define BRR_GB_D 4
+#endif
+constexpr int GB_D = BRR_GB_D;
+constexpr int GB_PITCH = GB_KC + 16;
+__host__ __device__ constexpr size_t gram_blk_buf(int NP) { return (size_t)2 * NP * GB_T * GB_PITCH; }
+__host__ __device__ constexpr size_t gram_blk_lds(int NP) { return 2 * gram_blk_buf(NP); }
+
+template <int NP>
+__global__ __launch_bounds__(512, 1) void k_gram_blk(Dev d, const uint8_t *Xk, const int *member, const int *bsz, int B,
+                                                     int nb, int shift, double *G, double *GT) {
+  static_assert(NP >= 1 && NP <= 2, "whole-tile accumulators for at most 2 explicit planes");
+  constexpr int NC = NP + 1;  // classes
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  uint8_t *stg = reinterpret_cast<uint8_t *>(gsm);  // [buffer][side][plane][column][row] indicator bytes
+  __shared__ int s_emin[2][GB_T];
+  __shared__ uint32_t s_cv[2][GB_T / 16];
+  __shared__ int s_h[2][GB_T][NC], s_M[2][GB_T][NC], s_E[2][GB_T][NC];
+  const int gb = blockIdx.x, gb2 = (gb + shift) % nb;
+  const int ntile = B / GB_T;
+  int ti = blockIdx.y / ntile, tj = blockIdx.y % ntile;
+  const bool mirror = shift == 0 && GT == nullptr;
+  if (mirror) {
+    int y = blockIdx.y;
+    ti = 0;
+    while (y >= ntile - ti) { y -= ntile - ti; ++ti; }
+    tj = ti + y;
+  }
+  const bool same = gb2 == gb && ti == tj;  // both sides the same columns: one expansion
+  const int bs = bsz[gb], bs2 = bsz[gb2];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, wi = wv >> 1, wj = wv & 1;
+  const int64_t N = d.N, nq = d.ldc;
+  if (t < 2 * GB_T / 16) s_cv[t / (GB_T / 16)][t % (GB_T / 16)] = 0u;
+  __syncthreads();
+  if (t < 2 * GB_T) {
+    const int side = t / GB_T, c = t % GB_T;
+    const int idx = (side ? tj : ti) * GB_T + c;
+    const int64_t col = idx < (side ? bs2 : bs) ? member[(int64_t)(side ? gb2 : gb) * B + idx] : -1;
+    const int nc = col >= 0 ? d.cls_info[col] & 7 : 0;  // (<= NC: d.gram_np is the cohort's most explicit planes)
+    if (col >= 0) atomicOr(&s_cv[side][c / 16], 1u << (c % 16));
+    int emin = 1 << 20, E[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const bool in = col >= 0 && k < nc;
+      const float v = in ? d.cls_val[4 * col + k] : 0.f;
+      s_h[side][c][k] = in ? d.cls_cnt[4 * col + k] : 0;
+      int e = 0;
+      const float f = frexpf(v, &e);
+      s_M[side][c][k] = v != 0.f ? (int)(f * 16777216.0f) : 0;
+      E[k] = e - 24;
+      if (v != 0.f) emin = min(emin, E[k]);
+    }
+    if (emin == (1 << 20)) emin = 0;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) s_E[side][c][k] = s_M[side][c][k] != 0 ? E[k] - emin : 0;
+    s_emin[side][c] = emin;
+  }
+  i32x4 acc[NP][NP][2][4];
+#pragma unroll
+  for (int a = 0; a < NP; ++a)
+#pragma unroll
+    for (int b = 0; b < NP; ++b)
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[a][b][x][y] = i32x4{0, 0, 0, 0};
+  // loader: per chunk of GB_KC rows, thread t the 16-B code group (side t >> 8, column group (t >> 5) & 7,
+  // row quad t & 31); side-1 threads idle when both sides are the same columns
+  constexpr int QPC = GB_KC / 4;
+  static_assert(2 * (GB_T / 16) * QPC == 512, "one element per thread and chunk");
+  const int eside = t >> 8, eq = (t >> 5) & 7, eg = t & 31;
+  const bool eon = !(same && eside == 1);
+  const int64_t nch = (N + GB_KC - 1) / GB_KC;
+  const uint4 *src = reinterpret_cast<const uint4 *>(Xk) +
+                     ((int64_t)(eside ? gb2 : gb) * (B / 16) + (eside ? tj : ti) * (GB_T / 16) + eq) * nq;
+  auto load = [&](int64_t ch) __attribute__((always_inline)) -> uint4 {
+    const int64_t c = ch < nch ? ch : nch - 1;
+    return src[min(c * QPC + eg, nq - 1)];
+  };
+  // expand (k_gram_int's bit spread) chunk ch's group into buffer bf: column 16 eq + 4 j + c, rows 4 eg .. 4 eg + 3
+  auto expand = [&](const uint4 &v, int64_t ch, uint8_t *bf) __attribute__((always_inline)) {
+    if (!eon) return;
+    const int64_t row4 = ch * GB_KC + 4 * eg;
+    const uint32_t vrow = row4 >= N ? 0u : row4 + 4 <= N ? 0x55u : (0x55u >> (2 * (int)(4 - (N - row4))));
+    const uint32_t cv = s_cv[eside][eq];
+    const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+    uint8_t *base = bf + ((eside * NP) * GB_T + 16 * eq) * GB_PITCH + 4 * eg;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t cb = (cv >> (4 * j)) & 0xFu;
+      const uint32_t cm = ((cb & 1u) ? 0xFFu : 0u) | ((cb & 2u) ? 0xFF00u : 0u) | ((cb & 4u) ? 0xFF0000u : 0u) |
+                          ((cb & 8u) ? 0xFF000000u : 0u);
+      const uint32_t m = cm & (vrow * 0x01010101u);
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const uint32_t e = ~(wd[j] ^ (0x55555555u * (uint32_t)p));
+        const uint32_t ind = e & (e >> 1) & m;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const uint32_t y = __builtin_amdgcn_ubfe(ind, 8 * c, 8);
+          *reinterpret_cast<uint32_t *>(base + (p * GB_T + 4 * j + c) * GB_PITCH) = (y * 0x41041u) & 0x01010101u;
+        }
+      }
+    }
+  };
+  uint4 ring[GB_D];  // ring[k]: the chunk of index = k (mod GB_D) next to be expanded
+#pragma unroll
+  for (int u = 0; u < GB_D; ++u) ring[u] = load(u);
+  __syncthreads();  // (the class tables, s_cv)
+  expand(ring[0], 0, stg);
+  ring[0] = load(GB_D);
+  __syncthreads();
+  for (int64_t c0 = 0; c0 < nch; c0 += GB_D) {
+#pragma unroll
+    for (int u = 0; u < GB_D; ++u) {
+      const int64_t ch = c0 + u;
+      if (ch >= nch) break;
+      // chunk ch + 1 into the other buffer (its last readers passed the barrier that ended chunk ch - 1)
+      if (ch + 1 < nch) {
+        expand(ring[(u + 1) % GB_D], ch + 1, stg + ((ch + 1) & 1) * gram_blk_buf(NP));
+        ring[(u + 1) % GB_D] = load(ch + 1 + GB_D);
+      }
+      const uint8_t *sa = stg + (ch & 1) * gram_blk_buf(NP);
+      const uint8_t *sb = same ? sa : sa + (size_t)NP * GB_T * GB_PITCH;
+#pragma unroll
+      for (int kk = 0; kk < GB_KC / 64; ++kk) {
+        i32x4 fa[NP][2], fb[NP][4];
+        const int ko = kk * 64 + 16 * (lane >> 4);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+#pragma unroll
+          for (int x = 0; x < 2; ++x)
+            fa[p][x] = *reinterpret_cast<const i32x4 *>(sa + (p * GB_T + 32 * wi + 16 * x + (lane & 15)) * GB_PITCH + ko);
+#pragma unroll
+          for (int y = 0; y < 4; ++y)
+            fb[p][y] = *reinterpret_cast<const i32x4 *>(sb + (p * GB_T + 64 * wj + 16 * y + (lane & 15)) * GB_PITCH + ko);
+        }
+#pragma unroll
+        for (int a = 0; a < NP; ++a)
+#pragma unroll
+          for (int b = 0; b < NP; ++b)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+              for (int y = 0; y < 4; ++y)
+                acc[a][b][x][y] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fa[a][x], fb[b][y], acc[a][b][x][y], 0, 0, 0);
+      }
+      __syncthreads();
+    }
+  }
+  // epilogue from the accumulators: element r of lane l of a 16 x 16 tile is (row 4 (l >> 4) + r, column l & 15)
+  double *g = G + (int64_t)gb * B * B;
+  double *gt = GT ? GT + (int64_t)gb * B * B : nullptr;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 32 * wi + 16 * x + 4 * (lane >> 4) + r, j = 64 * wj + 16 * y + (lane & 15);
+        const int ii = ti * GB_T + i, jj = tj * GB_T + j;
+        int64_t ne[NP][NP];
+#pragma unroll
+        for (int a = 0; a < NP; ++a)
+#pragma unroll
+          for (int b = 0; b < NP; ++b) ne[a][b] = acc[a][b][x][y][r];
+        // (entries past a short block's columns: 0, as k_gram_int writes them)
+        const double v = (ii < bs && jj < bs2) ? gram_entry<NP>(ne, s_h[0][i], s_h[1][j], s_M[0][i], s_M[1][j], s_E[0][i],
+                                                                s_E[1][j], s_emin[0][i], s_emin[1][j], N)
+                                               : 0.0;
+        g[(int64_t)ii * B + jj] = v;
+        if (gt) gt[(int64_t)jj * B + ii] = v;
+        if (mirror && ti != tj) g[(int64_t)jj * B + ii] = v;
+      }
+}
+
+// REFERENCE order (Dev::xcls, the column-major class codes, present) with at most 3 classes per column:
+// the same exact Gram blocks from fp4 planes on the block-scaled matrix cores, read straight from the
+// column-major codes (no per-sweep layout encoding, k_encode_gather).  Per column two planes of e2m1
+// values, the class code c (0, 1, 2) and c^2 (0, 1, 4) -- one plane c for 2 classes -- so the four plane
+// products S_pq = sum_rows c^p c'^q (p, q = 1, 2) are V n V^T with V = [[1, 2], [1, 4]] and n the class-pair
+// counts of classes 1 and 2 (invertible: 4 n is integer arithmetic on S); class 0 follows from the totals
+// (gram_entry's last class, the class tables stored in the order 1, 2, 0).  The f32 accumulators are exact
+// while 16 N < 2^24 (every product is an integer <= 16).  v_mfma_scale_f32_16x16x128_f8f6f4, unit scales:
+// twice the i8 form's K per instruction at the same cycles and half its operand bytes; lane l's operand is
+// row (column) l & 15, K = 32 (l >> 4) .. + 31 as 16 bytes, element 2q in the low nibble of byte q
+// (scripts/mb_fp4_layout.hip).  A thread expands 64 rows of one column (16 code bytes) into 32 bytes per
+// plane, two 16-B LDS stores each.  Tiles, waves and the epilogue as k_gram_blk.
+constexpr int GF_KC = 256;                  // rows per chunk
+constexpr int GF_PITCH = GF_KC / 2 + 16;    // bytes per column and plane (nibbles + pad)
+__host__ __device__ constexpr size_t gram_fp4_buf(int NP) { return (size_t)2 * NP * GB_T * GF_PITCH; }
+__host__ __device__ constexpr size_t gram_fp4_lds(int NP) { return 2 * gram_fp4_buf(NP); }
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// 8 rows' 2-bit class codes (16 bits) -> 8 nibbles, each code in the low two bits of its nibble
+__device__ __forceinline__ uint32_t spread2to4(uint32_t h) {
+  uint32_t x = h & 0xFFFFu;
+  x = (x | (x << 8)) & 0x00FF00FFu;
+  x = (x | (x << 4)) & 0x0F0F0F0Fu;
+  x = (x | (x << 2)) & 0x33333333u;
+  return x;
+}
+
+template <int NP>
+__global__ __launch_bounds__(512, 1) void k_gram_fp4(Dev d, const uint8_t *xcls, const int *member, const int *bsz, int B,
+                                                     int nb, int shift, double *G, double *GT) {
+  static_assert(NP >= 1 && NP <= 2, "planes c (and c^2) for at most 3 classes");
+  constexpr int NC = NP + 1;
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  uint8_t *stg = reinterpret_cast<uint8_t *>(gsm);  // [buffer][side][plane][column][row nibbles]
+  __shared__ int s_emin[2][GB_T];
+  __shared__ int s_h[2][GB_T][NC], s_M[2][GB_T][NC], s_E[2][GB_T][NC];  // slot (k + NP) % NC: class k
+  __shared__ int64_t s_col[2][GB_T];
+  const int gb = blockIdx.x, gb2 = (gb + shift) % nb;
+  const int ntile = B / GB_T;
+  int ti = blockIdx.y / ntile, tj = blockIdx.y % ntile;
+  const bool mirror = shift == 0 && GT == nullptr;
+  if (mirror) {
+    int y = blockIdx.y;
+    ti = 0;
+    while (y >= ntile - ti) { y -= ntile - ti; ++ti; }
+    tj = ti + y;
+  }
+  const bool same = gb2 == gb && ti == tj;
+  const int bs = bsz[gb], bs2 = bsz[gb2];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, wi = wv >> 1, wj = wv & 1;
+  const int64_t N = d.N, ldc = d.ldc;
+  if (t < 2 * GB_T) {
+    const int side = t / GB_T, c = t % GB_T;
+    const int idx = (side ? tj : ti) * GB_T + c;
+    const int64_t col = idx < (side ? bs2 : bs) ? member[(int64_t)(side ? gb2 : gb) * B + idx] : -1;
+    s_col[side][c] = col >= 0 ? col : 0;  // (a missing column reads column 0; its entries are written 0)
+    const int nc = col >= 0 ? d.cls_info[col] & 7 : 0;
+    int emin = 1 << 20, E[NC], Mv[NC], H[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const bool in = col >= 0 && k < nc;
+      const float v = in ? d.cls_val[4 * col + k] : 0.f;
+      H[k] = in ? d.cls_cnt[4 * col + k] : 0;
+      int e = 0;
+      const float f = frexpf(v, &e);
+      Mv[k] = v != 0.f ? (int)(f * 16777216.0f) : 0;
+      E[k] = e - 24;
+      if (v != 0.f) emin = min(emin, E[k]);
+    }
+    if (emin == (1 << 20)) emin = 0;
+#pragma unroll
+    for (int k = 0; k < NC; ++k) {
+      const int sl = (k + NP) % NC;
+      s_h[side][c][sl] = H[k];
+      s_M[side][c][sl] = Mv[k];
+      s_E[side][c][sl] = Mv[k] != 0 ? E[k] - emin : 0;
+    }
+    s_emin[side][c] = emin;
+  }
+  __syncthreads();
+  f32x4 acc[NP][NP][2][4];
+#pragma unroll
+  for (int a = 0; a < NP; ++a)
+#pragma unroll
+    for (int b = 0; b < NP; ++b)
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[a][b][x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // loader: per chunk and side, thread t the 16 code bytes (64 rows) part t & 3 of column t >> 2
+  const int ec = t >> 2, ep = t & 3;
+  const int nsd = same ? 1 : 2;
+  const int64_t nch = (N + GF_KC - 1) / GF_KC;  // (<= ldc / 64: ld is a multiple of 256)
+  const uint4 *src[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) src[k] = reinterpret_cast<const uint4 *>(xcls + s_col[k][ec] * ldc) + ep;
+  auto load = [&](int64_t ch, uint4 (&r)[2]) __attribute__((always_inline)) {
+    const int64_t c = (ch < nch ? ch : nch - 1) * (GF_KC / 64);
+    r[0] = src[0][c];
+    if (nsd == 2) r[1] = src[1][c];
+  };
+  auto expand = [&](const uint4 (&v)[2], uint8_t *bf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k >= nsd) break;
+      const uint32_t wd[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+      uint32_t pc[8], pq[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t lo = spread2to4(wd[q]), hi = spread2to4(wd[q] >> 16);
+        pc[2 * q] = lo << 1;
+        pc[2 * q + 1] = hi << 1;
+        pq[2 * q] = (lo << 1) | (lo & 0x22222222u);  // c^2: 2 -> 0110 (4.0), 1 -> 0010 (1.0)
+        pq[2 * q + 1] = (hi << 1) | (hi & 0x22222222u);
+      }
+      uint8_t *dst = bf + ((k * NP) * GB_T + ec) * GF_PITCH + 32 * ep;
+      *reinterpret_cast<uint4 *>(dst) = make_uint4(pc[0], pc[1], pc[2], pc[3]);
+      *reinterpret_cast<uint4 *>(dst + 16) = make_uint4(pc[4], pc[5], pc[6], pc[7]);
+      if (NP == 2) {
+        *reinterpret_cast<uint4 *>(dst + GB_T * GF_PITCH) = make_uint4(pq[0], pq[1], pq[2], pq[3]);
+        *reinterpret_cast<uint4 *>(dst + GB_T * GF_PITCH + 16) = make_uint4(pq[4], pq[5], pq[6], pq[7]);
+      }
+    }
+  };
+  uint4 ring[GB_D][2];
+#pragma unroll
+  for (int u = 0; u < GB_D; ++u) load(u, ring[u]);
+  expand(ring[0], stg);
+  load(GB_D, ring[0]);
+  __syncthreads();
+  for (int64_t c0 = 0; c0 < nch; c0 += GB_D) {
+#pragma unroll
+    for (int u = 0; u < GB_D; ++u) {
+      const int64_t ch = c0 + u;
+      if (ch >= nch) break;
+      if (ch + 1 < nch) {
+        expand(ring[(u + 1) % GB_D], stg + ((ch + 1) & 1) * gram_fp4_buf(NP));
+        load(ch + 1 + GB_D, ring[(u + 1) % GB_D]);
+      }
+      const uint8_t *sa = stg + (ch & 1) * gram_fp4_buf(NP);
+      const uint8_t *sb = same ? sa : sa + (size_t)NP * GB_T * GF_PITCH;
+#pragma unroll
+      for (int kk = 0; kk < GF_KC / 128; ++kk) {
+        i32x8 fa[NP][2], fb[NP][4];
+        const int ko = kk * 64 + 16 * (lane >> 4);
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+#pragma unroll
+          for (int x = 0; x < 2; ++x) {
+            const i32x4 v = *reinterpret_cast<const i32x4 *>(sa + (p * GB_T + 32 * wi + 16 * x + (lane & 15)) * GF_PITCH + ko);
+            fa[p][x] = i32x8{v.x, v.y, v.z, v.w, 0, 0, 0, 0};
+          }
+#pragma unroll
+          for (int y = 0; y < 4; ++y) {
+            const i32x4 v = *reinterpret_cast<const i32x4 *>(sb + (p * GB_T + 64 * wj + 16 * y + (lane & 15)) * GF_PITCH + ko);
+            fb[p][y] = i32x8{v.x, v.y, v.z, v.w, 0, 0, 0, 0};
+          }
+        }
+#pragma unroll
+        for (int a = 0; a < NP; ++a)
+#pragma unroll
+          for (int b = 0; b < NP; ++b)
+#pragma unroll
+            for (int x = 0; x < 2; ++x)
+#pragma unroll
+              for (int y = 0; y < 4; ++y)
+                acc[a][b][x][y] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fa[a][x], fb[b][y], acc[a][b][x][y], 4, 4, 0,
+                                                                                 0x7F7F7F7F, 0, 0x7F7F7F7F);
+      }
+      __syncthreads();
+    }
+  }
+  double *g = G + (int64_t)gb * B * B;
+  double *gt = GT ? GT + (int64_t)gb * B * B : nullptr;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 32 * wi + 16 * x + 4 * (lane >> 4) + r, j = 64 * wj + 16 * y + (lane & 15);
+        const int ii = ti * GB_T + i, jj = tj * GB_T + j;
+        int64_t ne[NP][NP];
+        if constexpr (NP == 1) {
+          ne[0][0] = (int64_t)acc[0][0][x][y][r];
+        } else {
+          // S = V n V^T, V = [[1, 2], [1, 4]]: U = 2 V^-1 S, 4 n = U (2 V^-T)
+          const int64_t S11 = (int64_t)acc[0][0][x][y][r], S12 = (int64_t)acc[0][1][x][y][r];
+          const int64_t S21 = (int64_t)acc[1][0][x][y][r], S22 = (int64_t)acc[1][1][x][y][r];
+          const int64_t U00 = 4 * S11 - 2 * S21, U01 = 4 * S12 - 2 * S22, U10 = S21 - S11, U11 = S22 - S12;
+          ne[0][0] = (4 * U00 - 2 * U01) / 4;
+          ne[0][1] = (U01 - U00) / 4;
+          ne[1][0] = (4 * U10 - 2 * U11) / 4;
+          ne[1][1] = (U11 - U10) / 4;
+        }
+        const double v = (ii < bs && jj < bs2) ? gram_entry<NP>(ne, s_h[0][i], s_h[1][j], s_M[0][i], s_M[1][j], s_E[0][i],
+                                                                s_E[1][j], s_emin[0][i], s_emin[1][j], N)
+                                               : 0.0;
+        g[(int64_t)ii * B + jj] = v;
+        if (gt) gt[(int64_t)jj * B + ii] = v;
+        if (mirror && ti != tj) g[(int64_t)jj * B + ii] = v;
+      }
+}
+
 __global__ void k_xsq_from_gram(const double *G, const int *member, const int *bsz, int B, int nb,
                                 double *xsq) {
   const int s = blockIdx.x;
@@ -4694,7 +5127,47 @@ static hipError_t launch_gram_int_t(const Dev &d, int shift, double *G, double *
   return hipGetLastError();
 }
 
+template <int NP>
+static hipError_t launch_gram_blk_t(const Dev &d, int shift, double *G, double *GT, hipStream_t st) {
+  constexpr size_t lds = gram_blk_lds(NP);
+  static const hipError_t attr =
+      hipFuncSetAttribute((const void *)k_gram_blk<NP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return attr;
+  const int nt = d.B / GB_T;
+  const int ntiles = (shift == 0 && GT == nullptr) ? nt * (nt + 1) / 2 : nt * nt;
+  hipLaunchKernelGGL((k_gram_blk<NP>), dim3((unsigned)d.nb, (unsigned)ntiles), dim3(512), lds, st, d, d.gram_codes,
+                     d.member, d.bsz, d.B, d.nb, shift, G, GT);
+  return hipGetLastError();
+}
+
+template <int NP>
+static hipError_t launch_gram_fp4_t(const Dev &d, int shift, double *G, double *GT, hipStream_t st) {
+  constexpr size_t lds = gram_fp4_lds(NP);
+  static const hipError_t attr =
+      hipFuncSetAttribute((const void *)k_gram_fp4<NP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (attr != hipSuccess) return attr;
+  const int nt = d.B / GB_T;
+  const int ntiles = (shift == 0 && GT == nullptr) ? nt * (nt + 1) / 2 : nt * nt;
+  hipLaunchKernelGGL((k_gram_fp4<NP>), dim3((unsigned)d.nb, (unsigned)ntiles), dim3(512), lds, st, d, d.xcls, d.member,
+                     d.bsz, d.B, d.nb, shift, G, GT);
+  return hipGetLastError();
+}
+
+// the fp4 Gram kernel applies: REFERENCE order's column-major class codes, at most 3 classes, whole
+// 128-column tiles, f32 sums exact (16 N < 2^24); BRR_GRAM_FP4=0 keeps the i8 kernels (A/B)
+bool gram_reads_xcls(const Dev &d) {
+  const char *f = getenv("BRR_GRAM_FP4");
+  return d.xcls && d.gram_np >= 1 && d.gram_np <= 2 && d.B % GB_T == 0 && d.ldc % 64 == 0 &&
+         16 * (int64_t)d.N < ((int64_t)1 << 24) && !(f && f[0] == '0');
+}
+
 hipError_t launch_gram(const Dev &d, int shift, double *G, double *GT, hipStream_t st) {
+  if (d.gram_np > 0 && gram_reads_xcls(d))
+    return d.gram_np == 1 ? launch_gram_fp4_t<1>(d, shift, G, GT, st) : launch_gram_fp4_t<2>(d, shift, G, GT, st);
+  // whole 128-column tiles for the genotype case (BRR_GRAM_TILE64=1: k_gram_int's 64-column tiles, A/B)
+  const char *t64 = getenv("BRR_GRAM_TILE64");
+  if (d.gram_np > 0 && d.gram_np <= 2 && d.gram_codes && d.B % GB_T == 0 && !(t64 && t64[0] == '1'))
+    return d.gram_np == 1 ? launch_gram_blk_t<1>(d, shift, G, GT, st) : launch_gram_blk_t<2>(d, shift, G, GT, st);
   if (d.gram_np > 0 && d.gram_codes && d.B % GI_T == 0) {
     switch (d.gram_np) {
       case 1: return launch_gram_int_t<1>(d, shift, G, GT, st);

@@ -24,6 +24,8 @@ hipError_t launch_encode_layout(const Dev &d, hipStream_t st);  // class codes o
 hipError_t launch_xcls(const Dev &d, uint8_t *xcls, hipStream_t st);  // column-major class codes (REFERENCE order)
 // Gram blocks: k_gram_int (exact, i8 matrix cores) when Dev::gram_np > 0, else k_gram (FP64 MFMA)
 hipError_t launch_gram(const Dev &d, int shift, double *G, double *GT, hipStream_t st);
+// the Gram blocks come from Dev::xcls (REFERENCE order, k_gram_fp4): no layout encoding needed
+bool gram_reads_xcls(const Dev &d);
 hipError_t launch_xsq(const Dev &d, hipStream_t st);
 hipError_t launch_rows(const Dev &d, int flags, const double *deps_in, hipStream_t st,
                        const double *eps_in = nullptr, int slot_a = -1, int slot_b = -1);

@@ -735,7 +735,7 @@ int prepare_classes(brr_session *s) {
 
 // Gram blocks of the current layout need its class codes first (k_gram_int)
 int encode_layout(brr_session *s) {
-  if (s->d.gram_np > 0) HIPCHK(launch_encode_layout(s->d, s->st));
+  if (s->d.gram_np > 0 && !gram_reads_xcls(s->d)) HIPCHK(launch_encode_layout(s->d, s->st));
   return 0;
 }
 

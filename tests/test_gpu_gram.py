@@ -62,11 +62,16 @@ def _genotypes(rng, N, P, nclass, zero_class=False):
     return X
 
 
+@pytest.mark.parametrize("tile", ["128", "64"])
 @pytest.mark.parametrize("storage", ["f32", "2bit"])
 @pytest.mark.parametrize("nclass,zero,N,B", [(3, False, 1003, 128), (2, False, 517, 64), (3, True, 1000, 128),
-                                             (3, False, 300, 256)])
-def test_integer_gram_is_correctly_rounded(brr, require_gpu, storage, nclass, zero, N, B):
+                                             (3, False, 300, 256), (2, False, 517, 128), (3, False, 201, 512)])
+def test_integer_gram_is_correctly_rounded(brr, require_gpu, monkeypatch, tile, storage, nclass, zero, N, B):
+    """tile 128: k_gram_blk (whole 128-column tiles, at most 2 explicit planes, B a multiple of 128; the
+    default there), 64: k_gram_int (BRR_GRAM_TILE64=1; every other case) -- both exact."""
     from bayesrrcpp_amd import _lib as L
+    if tile == "64":
+        monkeypatch.setenv("BRR_GRAM_TILE64", "1")
     rng = np.random.default_rng(nclass * 100 + N)
     P = 3 * B - 37  # a short last block
     X = _genotypes(rng, N, P, nclass, zero)
@@ -110,3 +115,60 @@ def test_fp64_and_integer_kernels_agree(brr, require_gpu, monkeypatch):
     assert np.max(np.abs(ga - gb)) <= 1e-12 * np.max(np.abs(ga))
     a.close()
     b.close()
+
+
+def _ref_session(brr, L, X, Y, B, storage):
+    N, P = X.shape
+    s = brr.Session(L.MODEL_V2, N, P, K=len(CVA) + 1, block_size=B, x_storage=storage, order_mode=L.ORDER_REFERENCE)
+    s.upload_x(X).set_y(Y).set_bayesr(**HYP, cva=CVA)
+    return s.init(3)
+
+
+@pytest.mark.parametrize("storage", ["f32", "2bit"])
+@pytest.mark.parametrize("nclass,N,B", [(3, 1003, 128), (2, 517, 128), (3, 300, 256)])
+def test_reference_order_fp4_gram_is_correctly_rounded(brr, require_gpu, storage, nclass, N, B):
+    """REFERENCE order reads the column-major class codes straight into fp4 planes (k_gram_fp4: planes c and
+    c^2 on the block-scaled matrix cores, class-pair counts recovered exactly): every block of the sweep's
+    layout (member order, vector ORDER) must again be the correctly rounded dot products, after init and
+    after a sweep's re-layout."""
+    from bayesrrcpp_amd import _lib as L
+    rng = np.random.default_rng(nclass * 1000 + N)
+    P = 3 * B - 37
+    X = _genotypes(rng, N, P, nclass)
+    Y = rng.standard_normal(N)
+    s = _ref_session(brr, L, X, Y, B, L.X_2BIT if storage == "2bit" else L.X_F32)
+    assert int(s.scalar(GRAM_NP)) == nclass - 1
+    nb = (P + B - 1) // B
+    for stage in range(2):
+        if stage:
+            s.sweep(1)
+        order = s.vector(L.ORDER).astype(np.int64)
+        G = s.vector(GRAM).reshape(nb, B, B)
+        XG = s.vector(XGRAM).reshape(nb, B, B)
+        blocks = [order[b * B:(b + 1) * B] for b in range(nb)]
+        for b in (0, nb - 1):
+            ca, cb = blocks[b], blocks[(b + 1) % nb]
+            ge = _exact_block(X, ca, ca)
+            assert np.array_equal(G[b][: len(ca), : len(ca)], ge), f"stage {stage} gram block {b}"
+            xge = _exact_block(X, ca, cb)
+            assert np.array_equal(XG[b][: len(ca), : len(cb)], xge), f"stage {stage} cross-Gram block {b}"
+    s.close()
+
+
+def test_reference_order_fp4_and_i8_chains_identical(brr, require_gpu, monkeypatch):
+    """The fp4 Gram kernel (default in REFERENCE order) and the i8 kernels (BRR_GRAM_FP4=0, with the per-sweep
+    layout encoding) give the same exact Gram blocks, so the chains are bit-identical."""
+    from bayesrrcpp_amd import _lib as L
+    rng = np.random.default_rng(5)
+    N, B = 1500, 128
+    X = _genotypes(rng, N, 5 * B - 9, 3)
+    Y = rng.standard_normal(N)
+    out = []
+    for fp4 in ("1", "0"):
+        monkeypatch.setenv("BRR_GRAM_FP4", fp4)
+        s = _ref_session(brr, L, X, Y, B, L.X_F32)
+        s.sweep(3)
+        out.append((s.vector(L.BETA), s.vector(L.EPS), s.vector(GRAM)))
+        s.close()
+    for a, b in zip(out[0], out[1]):
+        assert np.array_equal(a, b)
