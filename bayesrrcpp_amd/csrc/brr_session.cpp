@@ -455,6 +455,7 @@ int do_sweep_local(brr_session *s) {
       if (int rc = encode_layout(s)) return rc;
       HIPCHK(launch_gram(d, 0, d.gram, nullptr, s->st));
       HIPCHK(launch_gram(d, 1, d.xgram, d.xgramT, s->st));
+      if (d.lag >= 2) HIPCHK(launch_gram(d, 2, d.xgram2, d.xgram2T, s->st));  // (the layout's blocks two apart)
     } else {
       HIPCHK(launch_perm(d, it, s->shard, true, s->st));
     }
@@ -517,7 +518,10 @@ int do_sweep_local(brr_session *s) {
       // REFERENCE order 8.5 -> 6.7 (profiles/r06k_ab.log, r06h_ab.log).  BRR_OVS=0|1
       // overrides
       const char *ov = getenv("BRR_OVS");
-      dp.ovs = (ov ? ov[0] == '1' : s->model == MODEL_GROUPS) && ov_solver_ok(dp, s->fused);
+      // (default for Groups in BLOCKED order; REFERENCE order at lag 1 runs faster on the round-5 solver:
+  // 11.5 against 8.5 sweeps/s at C2, profiles/r06s_ab.log, r06v_ab.log)
+  dp.ovs = (ov ? ov[0] == '1' : (s->model == MODEL_GROUPS && s->order_mode == BRR_ORDER_BLOCKED)) &&
+           ov_solver_ok(dp, s->fused);
       if (dp.ovs) dp.rcorr = dp.rcsplit = dp.rcpf = 0;
       s->ovs_last = dp.ovs;
     }
@@ -1179,6 +1183,7 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
       int lag_pre = 1;
       if (opt.order_mode == BRR_ORDER_BLOCKED && s->nb >= 4 && !rows && !(pb && pb[0] == '1') && !(lg && atoi(lg) < 2))
         lag_pre = (lg && atoi(lg) >= 3 && s->nb >= 5) ? 3 : 2;
+      if (opt.order_mode == BRR_ORDER_REFERENCE && s->nb >= 4 && !rows && lg && atoi(lg) >= 2) lag_pre = 2;
       const double grams = (3.0 + 2.0 * (lag_pre - 1)) * 8.0 * (double)s->nb * B * B;
       // the integer Gram's class codes of the layout (N P / 4 bytes, during init; REFERENCE order keeps
       // them and a column-major copy for every sweep).  Without that memory init would fall back to
@@ -1304,9 +1309,12 @@ brr_session *brr_session_create(int32_t model, int64_t N, int64_t M, int64_t M_t
     // correction in the solver lag 2 was 25 / 7 % slower than lag 1 there), and for Groups (C3 12.41 ->
     // 12.58, profiles/r05j_ab.log).  BRR_LAG=1|2 overrides.
     const char *lg = getenv("BRR_LAG");
-    const bool lag2_ok = s->order_mode == BRR_ORDER_BLOCKED && s->nb >= 4;
+    // REFERENCE order only on request (BRR_LAG=2): its third Gram set per sweep (the layout's blocks two
+    // apart, ~14 ms with the fp4 Gram kernel) costs more than the deeper marker loop saves -- C2 in REFERENCE
+    // order 11.5 (lag 1) against 10.4 (lag 2; 10.8 with the overlapped solver), profiles/r06v_ab.log
+    const bool lag2_ok = (s->order_mode == BRR_ORDER_BLOCKED || (s->order_mode == BRR_ORDER_REFERENCE && lg)) && s->nb >= 4;
     d.lag = (lag2_ok && (lg ? atoi(lg) >= 2 : true)) ? 2 : 1;
-    if (d.lag == 2 && lg && atoi(lg) >= 3 && s->nb >= 5) d.lag = 3;  // (diagnostics: BRR_LAG=3)
+    if (d.lag == 2 && lg && atoi(lg) >= 3 && s->nb >= 5 && s->order_mode == BRR_ORDER_BLOCKED) d.lag = 3;  // (diagnostics: BRR_LAG=3)
     // row shards: the per-block kernels (the cross-shard sum of a block's dots sits between its
     // streaming and its solve; the fused sweep's in-kernel hand-over is one device's)
     // 2-bit storage in REFERENCE order: the fused streamers read a block's code tiles in storage

@@ -1002,3 +1002,37 @@ def test_overlapped_solver_both_ways(brr, oracle_mod, require_gpu, monkeypatch, 
         assert s.scalar(132) == ovs
         _compare(s, orc, O, L, model, tag=f"model={model} ovs={ovs} lag={lag} {xs} it={it}")
 
+
+
+@pytest.mark.parametrize("ovs", [0, 1])
+@pytest.mark.parametrize("model", [0, 1, 2])  # V2, Groups, restart
+def test_reference_order_lag2_matches_oracle(brr, oracle_mod, require_gpu, monkeypatch, model, ovs):
+    """REFERENCE order on the fused sweep at pipeline lag 2 (BRR_LAG=2: a third Gram set per sweep, the
+    layout's blocks two apart), with either solver, against the oracle's REFERENCE visit order
+    (BayesRv2.cpp:182 random_shuffle; BayesRv2Groups.cpp:232-298)."""
+    from bayesrrcpp_amd import _lib as L
+    O = oracle_mod
+    monkeypatch.setenv("BRR_OVS", str(ovs))
+    monkeypatch.setenv("BRR_LAG", "2")
+    monkeypatch.setenv("BRR_STREAM_WG", "5")
+    N, P = 1500, 1100
+    X, Y, _ = _cohort(O, N, P, n_causal=30)
+    kw = {}
+    if model == L.MODEL_GROUPS:
+        G = 3
+        kw = dict(G=G, gAssign=(np.arange(P) * G // P).astype(np.int32),
+                  fixed=np.linspace(-1, 1, N).reshape(N, 1))
+    elif model == L.MODEL_RESTART:
+        rng = np.random.default_rng(3)
+        comp0 = rng.integers(0, 4, P).astype(np.float64)
+        beta0 = np.where(comp0 > 0, rng.normal(0, 0.02, P), 0.0)
+        kw = dict(restart=dict(mu0=0.01, beta0=beta0, sigmaE0=0.7, sigmaGG0=np.array([0.3]),
+                               eps0=Y - X @ beta0 - 0.01, comp0=comp0))
+    s, orc = _make(brr, O, model, X, Y, 1, B=128, **kw)
+    assert s.scalar(104) > 1  # fused sweep
+    assert s.scalar(106) == 2  # pipeline lag
+    for it in range(4):
+        s.sweep(1)
+        orc.sweep(1)
+        assert s.scalar(132) == ovs
+        _compare(s, orc, O, L, model, tag=f"REFERENCE model={model} ovs={ovs} it={it}")
