@@ -1157,8 +1157,14 @@ __global__ __launch_bounds__(512, 1) void k_gram_blk(Dev d, const uint8_t *Xk, c
 // row (column) l & 15, K = 32 (l >> 4) .. + 31 as 16 bytes, element 2q in the low nibble of byte q
 // (scripts/mb_fp4_layout.hip).  A thread expands 64 rows of one column (16 code bytes) into 32 bytes per
 // plane, two 16-B LDS stores each.  Tiles, waves and the epilogue as k_gram_blk.
-constexpr int GF_KC = 256;                  // rows per chunk
-constexpr int GF_PITCH = GF_KC / 2 + 16;    // bytes per column and plane (nibbles + pad)
+constexpr int GF_KC = 256;               // rows per chunk
+constexpr int GF_PITCH = GF_KC / 2;      // bytes per column and plane (nibbles)
+// 16-B slot c of LDS row R at slot c ^ ((R >> 1) & 7) ^ (R & 1): the MFMA operand reads (ds_read_b128, lane l
+// row R = 16 m + (l & 15), slot 4 kk + (l >> 4)) are conflict-free in each of the instruction's 16-lane
+// groups (MI355X_MICROARCH.md LDS: groups {0-3, 12-15, 20-27}, ...; with 144-B rows, 2-way:
+// SQ_LDS_BANK_CONFLICT 1.2e9 cycles per call, profiles/r06x_gram_fp4_pmc.csv), and so are the expansion's
+// 16-B stores (8-lane groups: rows 2m and 2m + 1, slots of opposite parity)
+__device__ __forceinline__ int gf_slot(int R, int c) { return (c ^ ((R >> 1) & 7) ^ (R & 1)) << 4; }
 __host__ __device__ constexpr size_t gram_fp4_buf(int NP) { return (size_t)2 * NP * GB_T * GF_PITCH; }
 __host__ __device__ constexpr size_t gram_fp4_lds(int NP) { return 2 * gram_fp4_buf(NP); }
 typedef int i32x8 __attribute__((ext_vector_type(8)));
@@ -1239,13 +1245,16 @@ __global__ __launch_bounds__(512, 1) void k_gram_fp4(Dev d, const uint8_t *xcls,
   const int ec = t >> 2, ep = t & 3;
   const int nsd = same ? 1 : 2;
   const int64_t nch = (N + GF_KC - 1) / GF_KC;  // (<= ldc / 64: ld is a multiple of 256)
+  // (unconditional loads -- side 1 re-reads side 0's bytes when both are the same columns -- and no load
+  // under a branch: a load on one path of a branch makes the compiler drain every load at the join,
+  // i.e. the whole ring, before each chunk's products)
   const uint4 *src[2];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) src[k] = reinterpret_cast<const uint4 *>(xcls + s_col[k][ec] * ldc) + ep;
+  for (int k = 0; k < 2; ++k) src[k] = reinterpret_cast<const uint4 *>(xcls + s_col[same ? 0 : k][ec] * ldc) + ep;
   auto load = [&](int64_t ch, uint4 (&r)[2]) __attribute__((always_inline)) {
     const int64_t c = (ch < nch ? ch : nch - 1) * (GF_KC / 64);
     r[0] = src[0][c];
-    if (nsd == 2) r[1] = src[1][c];
+    r[1] = src[1][c];
   };
   auto expand = [&](const uint4 (&v)[2], uint8_t *bf) __attribute__((always_inline)) {
 #pragma unroll
@@ -1261,12 +1270,14 @@ __global__ __launch_bounds__(512, 1) void k_gram_fp4(Dev d, const uint8_t *xcls,
         pq[2 * q] = (lo << 1) | (lo & 0x22222222u);  // c^2: 2 -> 0110 (4.0), 1 -> 0010 (1.0)
         pq[2 * q + 1] = (hi << 1) | (hi & 0x22222222u);
       }
-      uint8_t *dst = bf + ((k * NP) * GB_T + ec) * GF_PITCH + 32 * ep;
-      *reinterpret_cast<uint4 *>(dst) = make_uint4(pc[0], pc[1], pc[2], pc[3]);
-      *reinterpret_cast<uint4 *>(dst + 16) = make_uint4(pc[4], pc[5], pc[6], pc[7]);
+      // slots 2 ep and 2 ep + 1 of row ec
+      uint8_t *row = bf + ((k * NP) * GB_T + ec) * GF_PITCH;
+      uint8_t *d0 = row + gf_slot(ec, 2 * ep), *d1 = row + gf_slot(ec, 2 * ep + 1);
+      *reinterpret_cast<uint4 *>(d0) = make_uint4(pc[0], pc[1], pc[2], pc[3]);
+      *reinterpret_cast<uint4 *>(d1) = make_uint4(pc[4], pc[5], pc[6], pc[7]);
       if (NP == 2) {
-        *reinterpret_cast<uint4 *>(dst + GB_T * GF_PITCH) = make_uint4(pq[0], pq[1], pq[2], pq[3]);
-        *reinterpret_cast<uint4 *>(dst + GB_T * GF_PITCH + 16) = make_uint4(pq[4], pq[5], pq[6], pq[7]);
+        *reinterpret_cast<uint4 *>(d0 + GB_T * GF_PITCH) = make_uint4(pq[0], pq[1], pq[2], pq[3]);
+        *reinterpret_cast<uint4 *>(d1 + GB_T * GF_PITCH) = make_uint4(pq[4], pq[5], pq[6], pq[7]);
       }
     }
   };
@@ -1281,16 +1292,15 @@ __global__ __launch_bounds__(512, 1) void k_gram_fp4(Dev d, const uint8_t *xcls,
     for (int u = 0; u < GB_D; ++u) {
       const int64_t ch = c0 + u;
       if (ch >= nch) break;
-      if (ch + 1 < nch) {
-        expand(ring[(u + 1) % GB_D], stg + ((ch + 1) & 1) * gram_fp4_buf(NP));
-        load(ch + 1 + GB_D, ring[(u + 1) % GB_D]);
-      }
+      // chunk ch + 1 (clamped: past the last chunk the other buffer is written and never read)
+      expand(ring[(u + 1) % GB_D], stg + ((ch + 1) & 1) * gram_fp4_buf(NP));
+      load(ch + 1 + GB_D, ring[(u + 1) % GB_D]);
       const uint8_t *sa = stg + (ch & 1) * gram_fp4_buf(NP);
       const uint8_t *sb = same ? sa : sa + (size_t)NP * GB_T * GF_PITCH;
 #pragma unroll
       for (int kk = 0; kk < GF_KC / 128; ++kk) {
         i32x8 fa[NP][2], fb[NP][4];
-        const int ko = kk * 64 + 16 * (lane >> 4);
+        const int ko = gf_slot(lane & 15, 4 * kk + (lane >> 4));  // (row bits 1-3 = those of lane & 15)
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
 #pragma unroll
