@@ -4208,6 +4208,9 @@ __device__ __forceinline__ void apply_staged(const Dev &d, int np, int nr, doubl
 // Dev::slab_storage).  The value tables of the block being consumed are staged in LDS in storage
 // order (s_lut, B entries) at each block boundary, after the previous block's last item and
 // before the barrier that precedes the first item of the block.
+#ifndef BRR_PF_DMA
+#define BRR_PF_DMA 1  // (diagnostics: 0 compiles the f32 list prefetch out)
+#endif
 template <int CW, int P, int XF, int NT = SWEEP_NT, bool PROF = false>
 __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int npass, double *eps_l, int *s_pidx,
                                             double *s_pbo, double *s_pbn, int *s_np, double *s_lut, int *s_mem,
@@ -4340,7 +4343,7 @@ __device__ __forceinline__ void stream_role(const Dev &d, int g, int rpw, int np
   int pf_m = 0, pf_np = 0, pf_nr = 0;
   double pf_d = 0.0;
   auto pf_step = [&](int s) __attribute__((always_inline)) {
-    if constexpr (!XF) {
+    if constexpr (!XF && BRR_PF_DMA) {
       const int a = s - LAG;  // the list boundary s + 1 applies
       if (pfe == 0 || pf_st >= 3 || s + 1 >= sb1 || a < sb0) return;
       const int slot = a % NSLOT;
