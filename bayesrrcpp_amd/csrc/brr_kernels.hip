@@ -3839,22 +3839,32 @@ __device__ __forceinline__ void apply_pending(const Dev &d, int slot, int64_t r0
     int col0 = ld_sc1_int(pidx + lane);
     int gi0 = XF ? ld_sc1_int(d.pend_gi + slot * d.pend_stride + lane) : 0;
     const double pd0 = ld_sc1(pbo + lane) - ld_sc1(pbn + lane);
+    // (B >= 128) entries 64 + lane in the same round trip, before the counts are known (the arrays hold
+    // B + 16 entries): a Horseshoe list -- every column of its block -- is staged in one round trip, not two
+    const bool two = d.B >= 128;
+    int col1 = two ? ld_sc1_int(pidx + 64 + lane) : 0;
+    int gi1 = (XF && two) ? ld_sc1_int(d.pend_gi + slot * d.pend_stride + 64 + lane) : 0;
+    const double pd1 = two ? ld_sc1(pbo + 64 + lane) - ld_sc1(pbn + 64 + lane) : 0.0;
     {
       // neutral padding entries (e >= nr: b_old = b_new = 0) take the last real entry's column: a
       // cache hit instead of column 0 from HBM, and no branch in the batched loads
-      const int src = lane < nr ? lane : max(nr - 1, 0);
-      col0 = __shfl(col0, src);
-      if (XF) gi0 = __shfl(gi0, src);
-      if (lane < np) {
-        s_pidx[lane] = col0;
+      const int last = max(nr - 1, 0);
+      const int lc0 = __shfl(col0, last & 63), lc1 = __shfl(col1, last & 63);
+      const int lg0 = XF ? __shfl(gi0, last & 63) : 0, lg1 = XF ? __shfl(gi1, last & 63) : 0;
+      const int lcol = last < 64 ? lc0 : lc1, lgi = last < 64 ? lg0 : lg1;
+      auto stage = [&](int e, int col, int gi, double pd) __attribute__((always_inline)) {
+        if (e >= nr) { col = lcol; gi = lgi; }
+        s_pidx[e] = col;
         if (XF) {
-          s_ppos[lane] = gi0;
-          s_cb[lane] = ccode ? (int64_t)(gi0 >> 4) * (npass * 64 * 16) + (gi0 & 15) : code_off(col0, 0, d.B, d.ldc);
+          s_ppos[e] = gi;
+          s_cb[e] = ccode ? (int64_t)(gi >> 4) * (npass * 64 * 16) + (gi & 15) : code_off(col, 0, d.B, d.ldc);
         }
-        s_pd[lane] = pd0;
-      }
+        s_pd[e] = pd;
+      };
+      if (lane < np) stage(lane, col0, gi0, pd0);
+      if (two && 64 + lane < np) stage(64 + lane, col1, gi1, pd1);
     }
-    for (int e = lane + 64; e < np; e += 64) {
+    for (int e = lane + (two ? 128 : 64); e < np; e += 64) {
       // neutral padding entries (b_old = b_new = 0) load the last real column again: a cache
       // hit instead of column 0 from HBM, and no branch in the batched loads
       const int es = e < nr ? e : max(nr - 1, 0);
