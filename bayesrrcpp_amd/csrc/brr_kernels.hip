@@ -1042,8 +1042,11 @@ __global__ __launch_bounds__(512, 1) void k_gram_blk(Dev d, const uint8_t *Xk, c
   const int eside = t >> 8, eq = (t >> 5) & 7, eg = t & 31;
   const bool eon = !(same && eside == 1);
   const int64_t nch = (N + GB_KC - 1) / GB_KC;
+  // (side-1 threads of a same-columns tile load side 0's groups and skip the expansion: no load under a
+  // branch, which would make the compiler drain the ring at the join -- see k_gram_fp4)
+  const int lside = same ? 0 : eside;
   const uint4 *src = reinterpret_cast<const uint4 *>(Xk) +
-                     ((int64_t)(eside ? gb2 : gb) * (B / 16) + (eside ? tj : ti) * (GB_T / 16) + eq) * nq;
+                     ((int64_t)(lside ? gb2 : gb) * (B / 16) + (lside ? tj : ti) * (GB_T / 16) + eq) * nq;
   auto load = [&](int64_t ch) __attribute__((always_inline)) -> uint4 {
     const int64_t c = ch < nch ? ch : nch - 1;
     return src[min(c * QPC + eg, nq - 1)];
@@ -1087,10 +1090,9 @@ __global__ __launch_bounds__(512, 1) void k_gram_blk(Dev d, const uint8_t *Xk, c
       const int64_t ch = c0 + u;
       if (ch >= nch) break;
       // chunk ch + 1 into the other buffer (its last readers passed the barrier that ended chunk ch - 1)
-      if (ch + 1 < nch) {
-        expand(ring[(u + 1) % GB_D], ch + 1, stg + ((ch + 1) & 1) * gram_blk_buf(NP));
-        ring[(u + 1) % GB_D] = load(ch + 1 + GB_D);
-      }
+      // chunk ch + 1 (clamped: past the last chunk the other buffer is written and never read)
+      expand(ring[(u + 1) % GB_D], ch + 1, stg + ((ch + 1) & 1) * gram_blk_buf(NP));
+      ring[(u + 1) % GB_D] = load(ch + 1 + GB_D);
       const uint8_t *sa = stg + (ch & 1) * gram_blk_buf(NP);
       const uint8_t *sb = same ? sa : sa + (size_t)NP * GB_T * GB_PITCH;
 #pragma unroll
